@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""Benchmark: decoded info-Mbps of the MI355X decoders (BASELINE.json metric).
+
+Headline (`value`): Polar N=1024 K=512 SCL L=8, 65 536 AWGN frames per GPU
+(BASELINE.json configs[1]); a step = one batched decode of the resident LLR
+matrix + on-device error count (+ one all-reduce of the counters when N > 1).
+Secondary (`ldpc`): LDPC (504,252) BP max_iter=20 (configs[2]) on the
+reference harness's frames (benchmarks/throughput_test.py:285-315: its encoder's
+invalid codewords, so every frame runs all 20 iterations).
+
+info-Mbps = frames * K_info / t / 1e6 (throughput_test.py:217, :304).
+Usage: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torchrun.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "decoded info-Mbps: polar N=1024 SCL L=8 & LDPC(504,252) BP, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def timed_steps(step, steps, warmup, world):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+class KernelTimer:
+    """HIP events around the decode launch, on the stream it is launched on."""
+
+    def __init__(self):
+        self.pairs = []
+
+    def __call__(self, fn):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        self.pairs.append((s, e))
+
+    def reset(self):
+        self.pairs = []
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        return float(np.mean([s.elapsed_time(e) for s, e in self.pairs])) if self.pairs else float("nan")
+
+
+def load_traffic(name):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p)).get(name)
+    except Exception:
+        return None
+
+
+def cpu_threads():
+    n = len(os.sched_getaffinity(0))
+    return max(1, min(16, n))
+
+
+def bench_polar(args, rank, world):
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.polar import SCLDecoder, construct_frozen_set
+
+    N, K, L, B = 1024, 512, args.list_size, args.batch
+    frozen = construct_frozen_set(N, K, 2.0)
+    dec = SCLDecoder(N, K, list_size=L, frozen_bits=frozen)
+    plan = dec.plan
+    off = rank * B
+    msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    _native.random_bits(42, off, msg)
+    cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+    _native.polar_encode(plan, msg, cw)
+    llr = AWGNChannel(args.snr).llr_batch_device(cw, N, B, seed=42, frame_offset=off)
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(3, dtype=torch.int64, device="cuda")
+    kt = KernelTimer()
+
+    def step():
+        kt(lambda: plan.decode(llr, out))
+        _native.count_errors(msg, out, K, counts)
+        if world > 1:
+            dist.all_reduce(counts)
+
+    dt = timed_steps(step, args.steps, args.warmup, world)
+    kms = kt.mean_ms()  # includes warmup launches; steady state
+    kt.reset()
+    for _ in range(3):
+        kt(lambda: plan.decode(llr, out))
+    kms = kt.mean_ms()
+    frames = B * world * args.steps
+    value = frames * K / dt / 1e6
+    bytes_per_frame = 8 * N + K
+    achieved = B * bytes_per_frame / (kms / 1e3) / 1e9
+    res = dict(value=value, ms_per_step=dt / args.steps * 1e3, kernel_ms=kms, B=B,
+               roofline=dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
+                             frac=achieved / HBM_PEAK_GBS, traffic=load_traffic("polar_scl_1024_l8"),
+                             algorithmic_bytes_per_frame=bytes_per_frame, frames_per_launch=B,
+                             kernel="polar_decode_kernel<8,false,%d>" % plan.info.fused_top,
+                             kernel_ms=kms),
+               plan=dict(lds_bytes=plan.info.lds_bytes, fused_top=plan.info.fused_top))
+    c = counts.cpu().numpy()
+    res["ber"] = float(c[0]) / max(1, c[2] * K)
+    res["fer"] = float(c[1]) / max(1, c[2])
+    if rank == 0 and world == 1 and not args.skip_cpu:
+        from oracle import oracle as O
+        S = args.cpu_frames
+        th = cpu_threads()
+        llr_h = llr[:S].cpu().numpy()
+        t0 = time.perf_counter()
+        ref = O.scl_decode(N, L, frozen, llr_h, threads=th)
+        ct = time.perf_counter() - t0
+        got = out[:S].cpu().numpy().astype(np.int64)
+        res["cpu_baseline"] = dict(value=S * K / ct / 1e6, unit="info-Mbps", cores=th, kind="port",
+                                   sample="first %d frames of the same LLR batch, oracle/refcpu.c SCL L=%d "
+                                          "(loop-faithful C restatement, OpenMP %d threads), %.1f s" % (S, L, th, ct),
+                                   mismatching_frames_vs_gpu=int((ref != got).any(axis=1).sum()))
+    return res
+
+
+def bench_ldpc(args, rank, world):
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.ldpc import BPDecoder, LDPCEncoder
+
+    n, k, B = 504, 252, args.batch
+    enc = LDPCEncoder(n, k, dv=3, dc=6, seed=42)  # throughput_test.py:285 (rank-251 H, direct solving)
+    dec = BPDecoder(enc.H, max_iter=20)
+    plan = dec.plan
+    rs = np.random.RandomState(42 + rank)
+    U = 4096  # distinct messages, tiled; every frame gets its own noise
+    base = enc.encode_batch(rs.randint(0, 2, (U, k)))
+    cw = torch.from_numpy(np.tile(base, (B // U + 1, 1))[:B].astype(np.uint8)).cuda()
+    llr = AWGNChannel(args.snr).llr_batch_device(cw, n, B, seed=4242, frame_offset=rank * B)
+    out = torch.empty((B, n), dtype=torch.uint8, device="cuda")
+    its = torch.empty((B,), dtype=torch.int32, device="cuda")
+    counts = torch.zeros(3, dtype=torch.int64, device="cuda")
+    kt = KernelTimer()
+
+    def step():
+        kt(lambda: plan.decode(llr, out, its))
+        _native_count(cw, out, k, counts)
+        if world > 1:
+            dist.all_reduce(counts)
+
+    from polarcode_and_ldpc_amd._native import count_errors as _native_count
+    dt = timed_steps(step, args.steps, args.warmup, world)
+    kt.reset()
+    for _ in range(3):
+        kt(lambda: plan.decode(llr, out, its))
+    kms = kt.mean_ms()
+    value = B * world * args.steps * k / dt / 1e6
+    bpf = 9 * n
+    achieved = B * bpf / (kms / 1e3) / 1e9
+    mean_it = float(its.double().mean().item())
+    res = dict(metric="decoded info-Mbps, LDPC (504,252) BP max_iter=20, reference-harness frames @ %.1f dB" % args.snr,
+               value=value, unit="info-Mbps", ms_per_step=dt / args.steps * 1e3, kernel_ms=kms,
+               mean_iterations=mean_it, vs_published=value / 7.95e-5,
+               roofline=dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
+                             frac=achieved / HBM_PEAK_GBS, traffic=load_traffic("ldpc_bp_504"),
+                             algorithmic_bytes_per_frame=bpf, frames_per_launch=B, kernel_ms=kms))
+    if rank == 0 and world == 1 and not args.skip_cpu:
+        from oracle import oracle as O
+        from polarcode_and_ldpc_amd.ldpc import dense_to_csr
+        S = args.cpu_frames_ldpc
+        th = cpu_threads()
+        rp, ci = dense_to_csr(enc.H)
+        llr_h = llr[:S].cpu().numpy()
+        t0 = time.perf_counter()
+        rb, ri = O.ldpc_decode(rp, ci, n, llr_h, "bp", 20, True, 1.0, threads=th)
+        ct = time.perf_counter() - t0
+        got = out[:S].cpu().numpy().astype(np.int64)
+        res["cpu_baseline"] = dict(value=S * k / ct / 1e6, unit="info-Mbps", cores=th, kind="port",
+                                   sample="first %d frames of the same batch, oracle/refcpu.c BP-20, %d threads, "
+                                          "%.1f s" % (S, th, ct),
+                                   mismatching_frames_vs_gpu=int((rb != got).any(axis=1).sum()))
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--list-size", type=int, default=8)
+    ap.add_argument("--snr", type=float, default=3.0)
+    ap.add_argument("--cpu-frames", type=int, default=512)
+    ap.add_argument("--cpu-frames-ldpc", type=int, default=2048)
+    ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--skip-ldpc", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    pol = bench_polar(args, rank, world)
+    ldp = None if args.skip_ldpc else bench_ldpc(args, rank, world)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": pol["value"], "unit": "info-Mbps", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": pol["ms_per_step"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: random messages, device polar encoder, device AWGN (Philox) at %.1f dB Es/N0" % args.snr,
+            "config": {"workload": "polar N=1024 K=512 SCL L=%d decode, bit-reversed Bhattacharyya(2 dB) frozen set"
+                                   % args.list_size,
+                       "global_batch": args.batch * world, "frames_per_gpu": args.batch,
+                       "parallelism": "frame-sharded x%d (one RCCL all-reduce of error counters per step)" % world},
+            "roofline": pol["roofline"],
+            "cpu_baseline": pol.get("cpu_baseline"),
+            "ber": pol["ber"], "fer": pol["fer"], "plan": pol["plan"],
+        }
+        if ldp is not None:
+            line["ldpc"] = ldp
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

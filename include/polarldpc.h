@@ -1,0 +1,118 @@
+/*
+ * polarldpc.h -- C-ABI of libpolarldpc.so, the MI355X (gfx950) batched
+ * channel decoder.  Plain pointers and sizes only; device pointers are
+ * hipMalloc'd (e.g. torch tensors' data_ptr()); `stream` is a hipStream_t
+ * passed as void* (NULL = legacy default stream).
+ *
+ * The reference (B1ear/PolarCode_and_LDPC) is pure Python/NumPy and has no FFI;
+ * each entry point below replaces the body of a reference Python method.  The
+ * Python drop-in classes (polarcode_and_ldpc_amd.polar.SCDecoder, ...) bind
+ * these with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Return codes: 0 ok, <0 error (PL_E*); pl_last_error() gives a thread-local
+ * message for the last failing call on the calling thread.
+ */
+#ifndef POLARLDPC_H
+#define POLARLDPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PL_OK 0
+#define PL_EINVAL (-1)       /* bad argument (reference: AssertionError)        */
+#define PL_ENOMEM (-2)       /* device allocation failed                         */
+#define PL_EHIP (-3)         /* HIP runtime error (launch, copy)                 */
+#define PL_EUNSUPPORTED (-4) /* valid for the reference but not for this build,  */
+                             /* or MS on a degree-1 check (reference ValueError) */
+
+#define PL_LDPC_BP 0 /* BPDecoder: sum-product, tanh rule   (src/ldpc/decoder.py:11-205)  */
+#define PL_LDPC_MS 1 /* MSDecoder: (normalised) min-sum     (src/ldpc/decoder.py:208-355) */
+
+typedef struct pl_plan pl_plan;
+
+typedef struct {
+    int32_t kind;       /* 0 polar, 1 ldpc                                         */
+    int32_t n_in;       /* LLRs per frame (N or n)                                 */
+    int32_t n_out;      /* output bits per frame: K (polar) or n (ldpc)            */
+    int32_t list_size;  /* polar: 0 = SC, >=1 = SCL list size                      */
+    int32_t lds_bytes;  /* dynamic LDS per workgroup of the decode kernel          */
+    int32_t fused_top;  /* polar: tree depths fused into the channel read (>=1)    */
+    int32_t frames_per_block; /* frames one workgroup decodes                     */
+    int32_t reserved;
+} pl_plan_info;
+
+/* Polar SC / SCL plan.
+ *   Replaces SCDecoder.__init__ (src/polar/decoder.py:16-36) when list_size == 0
+ *   and SCLDecoder.__init__ (src/polar/decoder.py:191-223) when list_size >= 1.
+ *   frozen_mask: host array [N], nonzero = frozen (the reference's frozen_bits
+ *   index set as a mask; info bits = the complement, ascending).
+ *   N power of two (2..32768); K = number of unfrozen positions, 1 <= K <= N
+ *   (the reference's 0 < K < N assertion, decoder.py:17-18, is made by the
+ *   Python layer on its K argument, exactly as the reference does). */
+int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_mask, int32_t list_size,
+                         int32_t flags, pl_plan** out);
+
+/* LDPC plan.  Replaces BPDecoder.__init__/_build_tanner_graph
+ *   (src/ldpc/decoder.py:18-60) for algo PL_LDPC_BP and MSDecoder.__init__
+ *   (:215-255) for PL_LDPC_MS.  H given as CSR over its m rows with ascending
+ *   column indices: row_ptr[m+1], col_idx[row_ptr[m]] (host arrays).
+ *   normalization is MSDecoder's factor (ignored for BP). */
+int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* col_idx,
+                        int32_t algo, int32_t max_iter, int32_t early_stop, double normalization,
+                        int32_t flags, pl_plan** out);
+
+/* Batched decode: replaces SCDecoder.decode (decoder.py:38-71),
+ *   SCLDecoder.decode (:225-262), BPDecoder.decode (src/ldpc/decoder.py:124-202)
+ *   and MSDecoder.decode (:289-352) applied to `batch` frames.
+ *   llr_dev : fp64 [batch][ld] device, row b = channel LLRs of frame b (n_in used)
+ *   bits_dev: uint8 [batch][n_out] device.  Polar: u_hat[info_bits] ascending;
+ *             LDPC: the full hard-decision word (decoded = total <= 0).
+ *   iters_dev: int32 [batch] device or NULL; LDPC: iterations run (BPDecoder's
+ *             return_iterations); polar: ignored.
+ *   Asynchronous on `stream`.  Deterministic (no atomics in the decode path). */
+int pl_decode(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
+              int32_t* iters_dev, void* stream);
+
+/* Pre-allocate the plan's device workspace for up to max_batch frames, so that
+ * pl_decode never allocates (needed before hipGraph capture of pl_decode). */
+int pl_plan_reserve(pl_plan* plan, int64_t max_batch);
+
+int pl_plan_get_info(const pl_plan* plan, pl_plan_info* info);
+int pl_plan_destroy(pl_plan* plan);
+const char* pl_last_error(void);
+
+/* ---- Monte-Carlo frame source (replaces src/channel/awgn.py:91-112 and the
+ *      message/encode loop of benchmarks/ber_simulation.py:167-177) ---------- */
+
+/* Random message bits, uint8 [batch][k], Philox4x32-10 keyed by (seed, global
+ * frame index = frame_offset + b): identical for any sharding of the frames. */
+int pl_random_bits(uint64_t seed, int64_t frame_offset, int64_t batch, int32_t k, uint8_t* bits_dev,
+                   void* stream);
+
+/* Polar encoder (src/polar/encoder.py:63-95 without CRC): u[info] = msg,
+ * u[frozen] = 0, x = u * F^{(x)n} (src/polar/utils.py:193-229).
+ * msg_dev uint8 [batch][K]; codeword_dev uint8 [batch][N]. */
+int pl_polar_encode(const pl_plan* plan, const uint8_t* msg_dev, int64_t batch, uint8_t* codeword_dev,
+                    void* stream);
+
+/* BPSK (0 -> +1, 1 -> -1) + AWGN with sigma = sqrt(1/(2*10^(snr_db/10)))
+ * (awgn.py:27-32, :47, :88), LLR = 2*y/sigma^2 (:75).  codeword_dev uint8
+ * [batch][n] or NULL for the all-zero codeword.  Noise: Philox4x32-10 keyed by
+ * (seed, frame_offset + b) + Box-Muller; statistically equivalent to the
+ * reference's np.random.normal, not stream-identical. */
+int pl_awgn_llr(const uint8_t* codeword_dev, int32_t n, int64_t batch, double snr_db, uint64_t seed,
+                int64_t frame_offset, double* llr_dev, int64_t ld, void* stream);
+
+/* Error counting (benchmarks/ber_simulation.py:180-189):
+ * counts_dev[0] += bit errors, [1] += frame errors, [2] += frames, over the
+ * first `width` entries of each row.  counts_dev int64[3], device. */
+int pl_count_errors(const uint8_t* ref_dev, int64_t ld_ref, const uint8_t* dec_dev, int64_t ld_dec,
+                    int32_t width, int64_t batch, int64_t* counts_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POLARLDPC_H */

@@ -1,0 +1,180 @@
+"""ctypes binding of libpolarldpc.so (include/polarldpc.h).
+
+The HIP library is the only compute path: if it is missing or cannot be
+loaded this module raises at import time -- there is no CPU fallback.
+PyTorch (ROCm) is used only to own device buffers and streams: it is imported
+first so that the library binds to the same HIP runtime instance as torch.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch  # noqa: F401  (loads torch's libamdhip64 first; our .so reuses it)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PL_LIB_PATH", os.path.join(_HERE, "_lib", "libpolarldpc.so"))
+
+PL_OK, PL_EINVAL, PL_ENOMEM, PL_EHIP, PL_EUNSUPPORTED = 0, -1, -2, -3, -4
+PL_LDPC_BP, PL_LDPC_MS = 0, 1
+
+EXPORTS = (
+    "pl_polar_plan_create", "pl_ldpc_plan_create", "pl_decode", "pl_plan_reserve", "pl_plan_get_info",
+    "pl_plan_destroy", "pl_last_error", "pl_random_bits", "pl_polar_encode", "pl_awgn_llr",
+    "pl_count_errors",
+)
+
+
+class PlanInfo(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("n_in", ctypes.c_int32), ("n_out", ctypes.c_int32),
+                ("list_size", ctypes.c_int32), ("lds_bytes", ctypes.c_int32), ("fused_top", ctypes.c_int32),
+                ("frames_per_block", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "polarcode_and_ldpc_amd: native library %s not found -- build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (make -C polarcode_and_ldpc_amd/csrc). "
+            "There is no CPU fallback." % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, I32, I64, D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+    PP = ctypes.POINTER(ctypes.c_void_p)
+    L.pl_polar_plan_create.argtypes = [I32, I32, P, I32, I32, PP]
+    L.pl_ldpc_plan_create.argtypes = [I32, I32, P, P, I32, I32, I32, D, I32, PP]
+    L.pl_decode.argtypes = [P, P, I64, I64, P, P, P]
+    L.pl_plan_reserve.argtypes = [P, I64]
+    L.pl_plan_get_info.argtypes = [P, ctypes.POINTER(PlanInfo)]
+    L.pl_plan_destroy.argtypes = [P]
+    L.pl_last_error.restype = ctypes.c_char_p
+    L.pl_random_bits.argtypes = [ctypes.c_uint64, I64, I64, I32, P, P]
+    L.pl_polar_encode.argtypes = [P, P, I64, P, P]
+    L.pl_awgn_llr.argtypes = [P, I32, I64, D, ctypes.c_uint64, I64, P, I64, P]
+    L.pl_count_errors.argtypes = [P, I64, P, I64, I32, I64, P, P]
+    for name in EXPORTS:
+        getattr(L, name).restype = ctypes.c_int if name != "pl_last_error" else ctypes.c_char_p
+    return L
+
+
+lib = _load()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str):
+    if rc == PL_OK:
+        return
+    msg = (lib.pl_last_error() or b"").decode(errors="replace")
+    if rc == PL_EINVAL:
+        raise AssertionError("%s: %s" % (what, msg))
+    if rc == PL_EUNSUPPORTED:
+        raise ValueError("%s: %s" % (what, msg))
+    raise NativeError("%s failed (%d): %s" % (what, rc, msg))
+
+
+def _stream(stream=None) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream) if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def _ld(t: "torch.Tensor") -> int:
+    """Row pitch in elements; a single row may carry any stride (e.g. 0 from a
+    NumPy newaxis view), so it is normalised to the row length."""
+    return int(t.stride(0)) if t.shape[0] > 1 else int(t.shape[1])
+
+
+def _dptr(t: "torch.Tensor"):
+    assert t.is_cuda and (t.dim() < 2 or t.stride(-1) == 1), "device tensor must have unit inner stride"
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("polarcode_and_ldpc_amd: no HIP device visible (the decoders run on MI355X only)")
+
+
+class Plan:
+    """Owner of a pl_plan*; immutable after creation."""
+
+    def __init__(self, handle: ctypes.c_void_p):
+        self._h = handle
+        info = PlanInfo()
+        check(lib.pl_plan_get_info(self._h, ctypes.byref(info)), "pl_plan_get_info")
+        self.info = info
+
+    @property
+    def handle(self):
+        return self._h
+
+    def reserve(self, max_batch: int):
+        check(lib.pl_plan_reserve(self._h, int(max_batch)), "pl_plan_reserve")
+
+    def decode(self, llr: "torch.Tensor", bits: "torch.Tensor", iters: "torch.Tensor | None" = None, stream=None):
+        """llr fp64 [B, >=n_in] (contiguous rows), bits uint8 [B, n_out], iters int32 [B] or None."""
+        assert llr.dtype == torch.float64 and llr.dim() == 2 and llr.stride(1) == 1
+        assert bits.dtype == torch.uint8 and bits.shape == (llr.shape[0], self.info.n_out)
+        B = llr.shape[0]
+        it = _dptr(iters) if iters is not None else None
+        check(lib.pl_decode(self._h, ctypes.c_void_p(llr.data_ptr()), B, _ld(llr), _dptr(bits), it,
+                            ctypes.c_void_p(_stream(stream))), "pl_decode")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.pl_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def polar_plan(N: int, K: int, frozen_mask: np.ndarray, list_size: int, flags: int = 0) -> Plan:
+    require_gpu()
+    mask = np.ascontiguousarray(frozen_mask, dtype=np.uint8)
+    h = ctypes.c_void_p()
+    check(lib.pl_polar_plan_create(int(N), int(K), mask.ctypes.data_as(ctypes.c_void_p), int(list_size),
+                                   int(flags), ctypes.byref(h)), "pl_polar_plan_create")
+    return Plan(h)
+
+
+def ldpc_plan(row_ptr: np.ndarray, col_idx: np.ndarray, n: int, algo: int, max_iter: int, early_stop: bool,
+              normalization: float = 1.0) -> Plan:
+    require_gpu()
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int32)
+    ci = np.ascontiguousarray(col_idx, dtype=np.int32)
+    h = ctypes.c_void_p()
+    check(lib.pl_ldpc_plan_create(len(rp) - 1, int(n), rp.ctypes.data_as(ctypes.c_void_p),
+                                  ci.ctypes.data_as(ctypes.c_void_p), int(algo), int(max_iter),
+                                  int(bool(early_stop)), float(normalization), 0, ctypes.byref(h)),
+          "pl_ldpc_plan_create")
+    return Plan(h)
+
+
+def random_bits(seed: int, frame_offset: int, bits: "torch.Tensor", stream=None):
+    B, k = bits.shape
+    check(lib.pl_random_bits(ctypes.c_uint64(seed & (2**64 - 1)), int(frame_offset), B, k, _dptr(bits),
+                             ctypes.c_void_p(_stream(stream))), "pl_random_bits")
+
+
+def polar_encode(plan: Plan, msg: "torch.Tensor", codeword: "torch.Tensor", stream=None):
+    check(lib.pl_polar_encode(plan.handle, _dptr(msg), msg.shape[0], _dptr(codeword),
+                              ctypes.c_void_p(_stream(stream))), "pl_polar_encode")
+
+
+def awgn_llr(codeword: "torch.Tensor | None", n: int, batch: int, snr_db: float, seed: int, frame_offset: int,
+             llr: "torch.Tensor", stream=None):
+    cw = _dptr(codeword) if codeword is not None else None
+    check(lib.pl_awgn_llr(cw, int(n), int(batch), float(snr_db), ctypes.c_uint64(seed & (2**64 - 1)),
+                          int(frame_offset), _dptr(llr), _ld(llr), ctypes.c_void_p(_stream(stream))),
+          "pl_awgn_llr")
+
+
+def count_errors(ref: "torch.Tensor", dec: "torch.Tensor", width: int, counts: "torch.Tensor", stream=None):
+    check(lib.pl_count_errors(_dptr(ref), _ld(ref), _dptr(dec), _ld(dec), int(width), ref.shape[0],
+                              _dptr(counts), ctypes.c_void_p(_stream(stream))), "pl_count_errors")

@@ -1,0 +1,292 @@
+// C-ABI of libpolarldpc.so (include/polarldpc.h): plan lifetime, argument
+// checking (mirroring the reference's assertions), dispatch to the kernels.
+#include "../../include/polarldpc.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "internal.hpp"
+
+struct pl_plan {
+    int kind = 0;  // 0 polar, 1 ldpc
+    int device = 0;
+    // polar
+    pl::PolarGeom pg{};
+    bool sc = false;
+    int list_size = 0;
+    uint32_t* d_frozen_dec = nullptr;  // decode-order frozen bitmask [ceil(N/32)]
+    int32_t* d_info_pos = nullptr;     // [K] ascending info indices
+    int32_t* d_pos2info = nullptr;     // [N] index -> info rank or -1
+    // ldpc
+    pl::LdpcGeom lg{};
+    pl::LdpcDev ld{};
+    int32_t* d_ldpc = nullptr;
+    double* work = nullptr;
+    int64_t work_frames = 0;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+static int hipfail(hipError_t e, const char* what) {
+    return fail(e == hipErrorOutOfMemory ? PL_ENOMEM : PL_EHIP,
+                std::string(what) + ": " + hipGetErrorString(e));
+}
+
+extern "C" const char* pl_last_error(void) { return g_err.c_str(); }
+
+static int bitrev(int v, int nb) {
+    int r = 0;
+    for (int i = 0; i < nb; ++i) { r = (r << 1) | (v & 1); v >>= 1; }
+    return r;
+}
+
+template <typename T>
+static hipError_t upload(T** dst, const std::vector<T>& src) {
+    const size_t bytes = (src.empty() ? 1 : src.size()) * sizeof(T);
+    hipError_t e = hipMalloc((void**)dst, bytes);
+    if (e != hipSuccess) return e;
+    if (!src.empty()) e = hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
+    return e;
+}
+
+static int env_int(const char* name, int dflt) {
+    const char* s = std::getenv(name);
+    return (s && *s) ? std::atoi(s) : dflt;
+}
+
+extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_mask, int32_t list_size,
+                                    int32_t flags, pl_plan** out) {
+    if (!out) return fail(PL_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (N < 2 || (N & (N - 1)) || N > (1 << pl::kMaxDepth))
+        return fail(PL_EINVAL, "N must be a power of 2 in [2, 32768]");
+    if (!(0 < K && K <= N)) return fail(PL_EINVAL, "K (info positions) must be in [1, N]");
+    if (list_size < 0) return fail(PL_EINVAL, "list_size must be >= 1 (0 = SC)");
+    if (list_size > 32) return fail(PL_EUNSUPPORTED, "list_size > 32 not supported by this build");
+    if (!frozen_mask) return fail(PL_EINVAL, "frozen_mask is NULL");
+    int n = 0;
+    while ((1 << n) < N) ++n;
+    std::vector<int32_t> info, pos2info(N, -1);
+    for (int j = 0; j < N; ++j)
+        if (!frozen_mask[j]) { pos2info[j] = (int32_t)info.size(); info.push_back(j); }
+    if ((int)info.size() != K) return fail(PL_EINVAL, "number of unfrozen positions != K");
+    std::vector<uint32_t> fdec((N + 31) / 32, 0u);
+    for (int i = 0; i < N; ++i)
+        if (frozen_mask[bitrev(i, n)]) fdec[i >> 5] |= 1u << (i & 31);
+
+    pl_plan* p = new pl_plan();
+    p->kind = 0;
+    p->sc = (list_size == 0);
+    p->list_size = list_size;
+    hipGetDevice(&p->device);
+    // fused-top depth: flags bits 0..3 (or env PL_POLAR_FUSED) override; else the
+    // smallest F whose LDS footprint fits the occupancy budget.
+    int F = flags & 0xF;
+    if (!F) F = env_int("PL_POLAR_FUSED", 0);
+    const int budget = env_int("PL_POLAR_LDS_BUDGET", 48 * 1024);
+    const int Lgeom = p->sc ? 1 : list_size;
+    if (!F) {
+        F = 0;
+        for (int f = 1; f <= 4 && f <= n; ++f) {
+            pl::PolarGeom g;
+            if (pl::polar_geom(N, K, Lgeom, f, &g) <= budget) { F = f; break; }
+        }
+        if (!F) {
+            for (int f = 1; f <= 4 && f <= n; ++f) {
+                pl::PolarGeom g;
+                if (pl::polar_geom(N, K, Lgeom, f, &g) <= 160 * 1024) { F = f; break; }
+            }
+        }
+        if (!F) { delete p; return fail(PL_EUNSUPPORTED, "decoder state exceeds LDS (N/list too large)"); }
+    }
+    if (F > 4) F = 4;
+    pl::polar_geom(N, K, Lgeom, F, &p->pg);
+    if (p->pg.lds_bytes > 160 * 1024) { delete p; return fail(PL_EUNSUPPORTED, "decoder state exceeds LDS"); }
+    hipError_t e;
+    if ((e = upload(&p->d_frozen_dec, fdec)) != hipSuccess ||
+        (e = upload(&p->d_info_pos, info)) != hipSuccess ||
+        (e = upload(&p->d_pos2info, pos2info)) != hipSuccess) {
+        pl_plan_destroy(p);
+        return hipfail(e, "plan upload");
+    }
+    if ((e = pl::polar_prepare(p->pg, p->sc)) != hipSuccess) {
+        pl_plan_destroy(p);
+        return hipfail(e, "hipFuncSetAttribute");
+    }
+    *out = p;
+    return PL_OK;
+}
+
+extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* col_idx,
+                                   int32_t algo, int32_t max_iter, int32_t early_stop, double normalization,
+                                   int32_t flags, pl_plan** out) {
+    (void)flags;
+    if (!out) return fail(PL_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (m < 0 || n < 1 || !row_ptr || (!col_idx && row_ptr[m] > 0)) return fail(PL_EINVAL, "bad H");
+    if (algo != PL_LDPC_BP && algo != PL_LDPC_MS) return fail(PL_EINVAL, "algo must be BP or MS");
+    if (max_iter < 1) return fail(PL_EINVAL, "max_iter must be >= 1");
+    const int E = row_ptr[m];
+    if (row_ptr[0] != 0 || E < 0) return fail(PL_EINVAL, "row_ptr[0] must be 0");
+    std::vector<int32_t> edge_chk(E), var_ptr(n + 1, 0), var_edge(E);
+    int maxdc = 0;
+    for (int c = 0; c < m; ++c) {
+        const int d = row_ptr[c + 1] - row_ptr[c];
+        if (d < 0) return fail(PL_EINVAL, "row_ptr not monotone");
+        if (d > maxdc) maxdc = d;
+        if (algo == PL_LDPC_MS && d == 1)
+            return fail(PL_EUNSUPPORTED, "min-sum on a degree-1 check (reference raises ValueError)");
+        for (int e = row_ptr[c]; e < row_ptr[c + 1]; ++e) {
+            if (col_idx[e] < 0 || col_idx[e] >= n) return fail(PL_EINVAL, "column index out of range");
+            if (e > row_ptr[c] && col_idx[e] <= col_idx[e - 1]) return fail(PL_EINVAL, "columns must ascend");
+            edge_chk[e] = c;
+            var_ptr[col_idx[e] + 1]++;
+        }
+    }
+    for (int v = 0; v < n; ++v) var_ptr[v + 1] += var_ptr[v];
+    int maxdv = 0;
+    for (int v = 0; v < n; ++v) maxdv = std::max(maxdv, var_ptr[v + 1] - var_ptr[v]);
+    if (maxdv > 128) return fail(PL_EUNSUPPORTED, "variable degree > 128");
+    {
+        std::vector<int32_t> fill(var_ptr.begin(), var_ptr.end() - 1);
+        for (int c = 0; c < m; ++c)
+            for (int e = row_ptr[c]; e < row_ptr[c + 1]; ++e) var_edge[fill[col_idx[e]]++] = e;
+    }
+    pl_plan* p = new pl_plan();
+    p->kind = 1;
+    hipGetDevice(&p->device);
+    pl::LdpcGeom& g = p->lg;
+    g.m = m; g.n = n; g.E = E; g.max_iter = max_iter; g.early_stop = early_stop ? 1 : 0; g.algo = algo;
+    g.maxdc = maxdc; g.maxdv = maxdv; g.norm = normalization;
+    g.threads = E <= 4096 ? 256 : 1024;
+    const size_t lds_all = (size_t)(2 * (size_t)E + n) * 8 + n;
+    g.use_global = lds_all > 64 * 1024 ? 1 : 0;
+    g.lds_bytes = (int)(((g.use_global ? (size_t)n : lds_all) + 15) & ~(size_t)15);
+    std::vector<int32_t> all;
+    all.insert(all.end(), row_ptr, row_ptr + m + 1);
+    all.insert(all.end(), col_idx, col_idx + E);
+    all.insert(all.end(), edge_chk.begin(), edge_chk.end());
+    all.insert(all.end(), var_ptr.begin(), var_ptr.end());
+    all.insert(all.end(), var_edge.begin(), var_edge.end());
+    hipError_t e = upload(&p->d_ldpc, all);
+    if (e != hipSuccess) { pl_plan_destroy(p); return hipfail(e, "plan upload"); }
+    p->ld.row_ptr = p->d_ldpc;
+    p->ld.col_idx = p->ld.row_ptr + (m + 1);
+    p->ld.edge_chk = p->ld.col_idx + E;
+    p->ld.var_ptr = p->ld.edge_chk + E;
+    p->ld.var_edge = p->ld.var_ptr + (n + 1);
+    if ((e = pl::ldpc_prepare(g)) != hipSuccess) { pl_plan_destroy(p); return hipfail(e, "hipFuncSetAttribute"); }
+    *out = p;
+    return PL_OK;
+}
+
+static int reserve(pl_plan* p, int64_t frames) {
+    if (p->kind != 1 || !p->lg.use_global || frames <= p->work_frames) return PL_OK;
+    if (p->work) { hipFree(p->work); p->work = nullptr; p->work_frames = 0; }
+    const size_t bytes = pl::ldpc_work_bytes_per_frame(p->lg) * (size_t)frames;
+    hipError_t e = hipMalloc((void**)&p->work, bytes);
+    if (e != hipSuccess) return hipfail(e, "workspace");
+    p->work_frames = frames;
+    return PL_OK;
+}
+
+extern "C" int pl_plan_reserve(pl_plan* p, int64_t max_batch) {
+    if (!p) return fail(PL_EINVAL, "plan is NULL");
+    const int64_t chunk = env_int("PL_LDPC_CHUNK", 16384);
+    return reserve(p, max_batch < chunk ? max_batch : chunk);
+}
+
+extern "C" int pl_decode(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
+                         int32_t* iters, void* stream) {
+    if (!p) return fail(PL_EINVAL, "plan is NULL");
+    if (batch < 0) return fail(PL_EINVAL, "batch < 0");
+    if (batch == 0) return PL_OK;
+    if (!llr || !bits) return fail(PL_EINVAL, "NULL buffer");
+    hipStream_t s = (hipStream_t)stream;
+    if (p->kind == 0) {
+        if (ld < p->pg.N) return fail(PL_EINVAL, "ld < N");
+        hipError_t e = pl::polar_launch(p->pg, p->sc, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, s);
+        if (e != hipSuccess) return hipfail(e, "polar decode launch");
+        return PL_OK;
+    }
+    if (ld < p->lg.n) return fail(PL_EINVAL, "ld < n");
+    if (!p->lg.use_global) {
+        hipError_t e = pl::ldpc_launch(p->lg, p->ld, llr, ld, bits, iters, batch, nullptr, s);
+        return e == hipSuccess ? PL_OK : hipfail(e, "ldpc decode launch");
+    }
+    const int64_t chunk = env_int("PL_LDPC_CHUNK", 16384);
+    int rc = reserve(p, batch < chunk ? batch : chunk);
+    if (rc) return rc;
+    for (int64_t b0 = 0; b0 < batch; b0 += p->work_frames) {
+        const int64_t nb = std::min<int64_t>(p->work_frames, batch - b0);
+        hipError_t e = pl::ldpc_launch(p->lg, p->ld, llr + b0 * ld, ld, bits + b0 * p->lg.n,
+                                       iters ? iters + b0 : nullptr, nb, p->work, s);
+        if (e != hipSuccess) return hipfail(e, "ldpc decode launch");
+    }
+    return PL_OK;
+}
+
+extern "C" int pl_plan_get_info(const pl_plan* p, pl_plan_info* info) {
+    if (!p || !info) return fail(PL_EINVAL, "NULL argument");
+    *info = pl_plan_info{};
+    if (p->kind == 0) {
+        info->kind = 0; info->n_in = p->pg.N; info->n_out = p->pg.K; info->list_size = p->list_size;
+        info->lds_bytes = p->pg.lds_bytes; info->fused_top = p->pg.F; info->frames_per_block = 1;
+    } else {
+        info->kind = 1; info->n_in = p->lg.n; info->n_out = p->lg.n; info->list_size = 0;
+        info->lds_bytes = p->lg.lds_bytes; info->fused_top = 0; info->frames_per_block = 1;
+    }
+    return PL_OK;
+}
+
+extern "C" int pl_plan_destroy(pl_plan* p) {
+    if (!p) return PL_OK;
+    if (p->d_frozen_dec) hipFree(p->d_frozen_dec);
+    if (p->d_info_pos) hipFree(p->d_info_pos);
+    if (p->d_pos2info) hipFree(p->d_pos2info);
+    if (p->d_ldpc) hipFree(p->d_ldpc);
+    if (p->work) hipFree(p->work);
+    delete p;
+    return PL_OK;
+}
+
+extern "C" int pl_random_bits(uint64_t seed, int64_t frame_offset, int64_t batch, int32_t k, uint8_t* bits,
+                              void* stream) {
+    if (batch < 0 || k < 0 || (!bits && batch * k > 0)) return fail(PL_EINVAL, "bad argument");
+    hipError_t e = pl::random_bits_launch(seed, frame_offset, batch, k, bits, (hipStream_t)stream);
+    return e == hipSuccess ? PL_OK : hipfail(e, "random bits launch");
+}
+
+extern "C" int pl_polar_encode(const pl_plan* p, const uint8_t* msg, int64_t batch, uint8_t* cw, void* stream) {
+    if (!p || p->kind != 0) return fail(PL_EINVAL, "not a polar plan");
+    if (batch < 0 || (batch > 0 && (!msg || !cw))) return fail(PL_EINVAL, "bad argument");
+    hipError_t e = pl::polar_encode_launch(p->pg.N, p->pg.K, p->d_pos2info, msg, batch, cw, (hipStream_t)stream);
+    return e == hipSuccess ? PL_OK : hipfail(e, "polar encode launch");
+}
+
+extern "C" int pl_awgn_llr(const uint8_t* cw, int32_t n, int64_t batch, double snr_db, uint64_t seed,
+                           int64_t frame_offset, double* llr, int64_t ld, void* stream) {
+    if (n < 1 || batch < 0 || ld < n || (!llr && batch > 0)) return fail(PL_EINVAL, "bad argument");
+    // src/channel/awgn.py:27-32 -- same double-precision expression order
+    const double snr_linear = std::pow(10.0, snr_db / 10.0);
+    const double sigma = std::sqrt(1.0 / (2.0 * snr_linear));
+    const double sigma2 = sigma * sigma;
+    hipError_t e = pl::awgn_launch(cw, n, batch, sigma, sigma2, seed, frame_offset, llr, ld, (hipStream_t)stream);
+    return e == hipSuccess ? PL_OK : hipfail(e, "awgn launch");
+}
+
+extern "C" int pl_count_errors(const uint8_t* ref, int64_t ldr, const uint8_t* dec, int64_t ldd, int32_t width,
+                               int64_t batch, int64_t* counts, void* stream) {
+    if (batch < 0 || width < 0 || !counts || (batch > 0 && (!ref || !dec))) return fail(PL_EINVAL, "bad argument");
+    hipError_t e = pl::count_errors_launch(ref, ldr, dec, ldd, width, batch, counts, (hipStream_t)stream);
+    return e == hipSuccess ? PL_OK : hipfail(e, "count errors launch");
+}

@@ -1,0 +1,158 @@
+// Monte-Carlo frame source and error counting on the device.
+//   random message bits  : benchmarks/ber_simulation.py:169 (np.random.randint)
+//   polar encoder        : src/polar/encoder.py:63-95, src/polar/utils.py:193-229
+//   AWGN + BPSK + LLR    : src/channel/awgn.py:27-32, :47, :75, :88, :91-112
+//   error counting       : benchmarks/ber_simulation.py:180-189
+// Randomness: Philox4x32-10 keyed by (seed, global frame index), so a frame's
+// noise does not depend on how frames are sharded over launches or GPUs.
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace pl {
+
+// one thread per 32 message bits
+__global__ void random_bits_kernel(uint64_t seed, int64_t off, int64_t batch, int k, uint8_t* bits) {
+    const int wpf = (k + 31) / 32;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= batch * wpf) return;
+    const int64_t b = idx / wpf;
+    const int w = (int)(idx % wpf);
+    const uint64_t f = (uint64_t)(off + b);
+    const pl_u4 r = philox4x32_10(pl_u4{(uint32_t)w, (uint32_t)f, (uint32_t)(f >> 32), 0xB175B175u},
+                                  (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint32_t x = r.x;
+    uint8_t* o = bits + b * k + w * 32;
+    const int cnt = (k - w * 32) < 32 ? (k - w * 32) : 32;
+    for (int j = 0; j < cnt; ++j) o[j] = (x >> j) & 1u;
+}
+
+// one wavefront per frame: u by ballot over N positions, transform in LDS.
+__global__ void __launch_bounds__(64)
+polar_encode_kernel(int N, int K, const int32_t* __restrict__ pos2info, const uint8_t* __restrict__ msg,
+                    int64_t batch, uint8_t* __restrict__ cw) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* X = reinterpret_cast<uint32_t*>(smem);
+    const int64_t b = blockIdx.x;
+    if (b >= batch) return;
+    const int lane = threadIdx.x;
+    const int words = N < 32 ? 1 : N / 32;
+    const uint8_t* m = msg + b * K;
+    for (int base = 0; base < N; base += 64) {
+        const int j = base + lane;
+        int bitv = 0;
+        if (j < N) {
+            const int k = pos2info[j];
+            bitv = (k >= 0) ? (m[k] & 1) : 0;
+        }
+        const unsigned long long bal = __ballot(bitv);
+        if (lane == 0) {
+            X[base / 32] = (uint32_t)bal;
+            if (base / 32 + 1 < words) X[base / 32 + 1] = (uint32_t)(bal >> 32);
+        }
+    }
+    __syncthreads();
+    for (int w = lane; w < words; w += 64) X[w] = polar_word_transform(X[w]);
+    for (int sw = 1; sw < words; sw <<= 1) {
+        __syncthreads();
+        for (int w = lane; w < words; w += 64)
+            if (!(w & sw)) X[w] ^= X[w + sw];
+    }
+    __syncthreads();
+    uint8_t* o = cw + b * N;
+    for (int j = lane; j < N; j += 64) o[j] = (X[j >> 5] >> (j & 31)) & 1u;
+}
+
+// two LLRs per thread (one Philox call -> two 53-bit uniforms -> Box-Muller pair)
+__global__ void awgn_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch, double sigma,
+                            double sigma2, uint64_t seed, int64_t off, double* __restrict__ llr, int64_t ld) {
+    const int ppf = (n + 1) / 2;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= batch * ppf) return;
+    const int64_t b = idx / ppf;
+    const int q = (int)(idx % ppf);
+    const uint64_t f = (uint64_t)(off + b);
+    const pl_u4 r = philox4x32_10(pl_u4{(uint32_t)q, (uint32_t)f, (uint32_t)(f >> 32), 0xA3A3A3A3u},
+                                  (uint32_t)seed ^ 0x5bd1e995u, (uint32_t)(seed >> 32));
+    const uint64_t a = ((uint64_t)r.y << 32) | r.x, c = ((uint64_t)r.w << 32) | r.z;
+    const double u1 = ((double)(a >> 11) + 1.0) * 0x1.0p-53;  // (0, 1]
+    const double u2 = (double)(c >> 11) * 0x1.0p-53;           // [0, 1)
+    const double rad = sqrt(-2.0 * log(u1));
+    double sn, cs;
+    sincospi(2.0 * u2, &sn, &cs);
+    const double z[2] = {rad * cs, rad * sn};
+    double* o = llr + b * ld;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j = 2 * q + h;
+        if (j < n) {
+            const double s = cw ? 1.0 - 2.0 * (double)cw[b * n + j] : 1.0;  // awgn.py:47
+            const double y = s + sigma * z[h];                              // awgn.py:88
+            o[j] = 2.0 * y / sigma2;                                        // awgn.py:75
+        }
+    }
+}
+
+// one wavefront per frame; per-block partial sums -> 3 integer atomics
+__global__ void __launch_bounds__(256)
+count_errors_kernel(const uint8_t* __restrict__ ref, int64_t ldr, const uint8_t* __restrict__ dec,
+                    int64_t ldd, int width, int64_t batch, int64_t* counts) {
+    __shared__ unsigned long long part[2][4];
+    const int wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+    unsigned long long be = 0, fe = 0;
+    for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < batch; b += (int64_t)gridDim.x * 4) {
+        int e = 0;
+        for (int j = lane; j < width; j += 64) e += (ref[b * ldr + j] & 1) != (dec[b * ldd + j] & 1);
+        for (int s = 32; s > 0; s >>= 1) e += __shfl_xor(e, s);
+        be += (unsigned)e;
+        fe += e > 0 ? 1 : 0;
+    }
+    if (lane == 0) { part[0][wave] = be; part[1][wave] = fe; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long sb = 0, sf = 0;
+        for (int w = 0; w < 4; ++w) { sb += part[0][w]; sf += part[1][w]; }
+        atomicAdd(reinterpret_cast<unsigned long long*>(counts + 0), sb);
+        atomicAdd(reinterpret_cast<unsigned long long*>(counts + 1), sf);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(counts + 2), (unsigned long long)batch);
+}
+
+hipError_t random_bits_launch(uint64_t seed, int64_t off, int64_t batch, int k, uint8_t* bits,
+                              hipStream_t s) {
+    const int64_t tot = batch * ((k + 31) / 32);
+    if (tot == 0) return hipSuccess;
+    hipLaunchKernelGGL(random_bits_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seed, off,
+                       batch, k, bits);
+    return hipGetLastError();
+}
+
+hipError_t polar_encode_launch(int N, int K, const int32_t* pos2info, const uint8_t* msg, int64_t batch,
+                               uint8_t* cw, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    const int words = N < 32 ? 1 : N / 32;
+    hipLaunchKernelGGL(polar_encode_kernel, dim3((unsigned)batch), dim3(64), words * 4 + 8, s, N, K, pos2info,
+                       msg, batch, cw);
+    return hipGetLastError();
+}
+
+hipError_t awgn_launch(const uint8_t* cw, int n, int64_t batch, double sigma, double sigma2, uint64_t seed,
+                       int64_t off, double* llr, int64_t ld, hipStream_t s) {
+    const int64_t tot = batch * ((n + 1) / 2);
+    if (tot == 0) return hipSuccess;
+    hipLaunchKernelGGL(awgn_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, cw, n, batch, sigma,
+                       sigma2, seed, off, llr, ld);
+    return hipGetLastError();
+}
+
+hipError_t count_errors_launch(const uint8_t* ref, int64_t ldr, const uint8_t* dec, int64_t ldd, int width,
+                               int64_t batch, int64_t* counts, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    int64_t blocks = (batch + 3) / 4;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(count_errors_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ref, ldr, dec, ldd, width,
+                       batch, counts);
+    return hipGetLastError();
+}
+
+}  // namespace pl

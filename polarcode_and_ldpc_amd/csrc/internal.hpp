@@ -1,0 +1,59 @@
+// Host-side internal interface between the C-ABI (capi.cpp) and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pl {
+
+constexpr int kMaxDepth = 15;  // N <= 2^15
+
+// LDS layout of one frame's list-decoder state (one wave = one frame).
+struct PolarGeom {
+    int N, n, K, Lsz, F, lcap;
+    int lds_bytes;
+    int cw;                    // words of the transform / walk scratch (max(1, N/32))
+    int llr_off[kMaxDepth + 2];  // byte offset of the LLR pool at depth d (F <= d < n)
+    int bl_off[kMaxDepth + 2];   // byte offset of the left-beta pool at depth d (1 <= d <= n)
+    int bl_words[kMaxDepth + 2]; // u32 words per slot at depth d
+    int cur_off;               // [lcap][2][cw] u32 ping-pong walk scratch
+    int tab_off;               // [lcap][32] bytes: LLR slot ptr [0..15], beta slot ptr [16..31]
+    int surv_off;              // [lcap] x 16 B survivor table
+};
+
+int polar_lcap(int list_size);  // lane-group count (power of two) for a list size
+int polar_geom(int N, int K, int list_size, int F, PolarGeom* g);  // fills layout, returns lds bytes
+hipError_t polar_launch(const PolarGeom& g, bool sc, const double* llr, int64_t ld, uint8_t* out,
+                        const uint32_t* frozen_dec, const int32_t* info_pos, int64_t batch,
+                        hipStream_t s);
+hipError_t polar_prepare(const PolarGeom& g, bool sc);  // raise the kernel's LDS limit
+
+hipError_t polar_encode_launch(int N, int K, const int32_t* pos2info, const uint8_t* msg,
+                               int64_t batch, uint8_t* cw, hipStream_t s);
+hipError_t random_bits_launch(uint64_t seed, int64_t off, int64_t batch, int k, uint8_t* bits,
+                              hipStream_t s);
+hipError_t awgn_launch(const uint8_t* cw, int n, int64_t batch, double sigma, double sigma2,
+                       uint64_t seed, int64_t off, double* llr, int64_t ld, hipStream_t s);
+hipError_t count_errors_launch(const uint8_t* ref, int64_t ldr, const uint8_t* dec, int64_t ldd,
+                               int width, int64_t batch, int64_t* counts, hipStream_t s);
+
+// ---- LDPC ----
+struct LdpcGeom {
+    int m, n, E, max_iter, early_stop, algo, maxdc, maxdv;
+    double norm;
+    int threads;       // threads per workgroup (one frame per workgroup)
+    int lds_bytes;     // 0 => messages live in the global workspace
+    int use_global;
+};
+struct LdpcDev {
+    const int32_t* row_ptr;   // [m+1]
+    const int32_t* col_idx;   // [E]   (check-major edge -> variable)
+    const int32_t* edge_chk;  // [E]   edge -> check
+    const int32_t* var_ptr;   // [n+1]
+    const int32_t* var_edge;  // [E]   var-major list of check-major edge ids (ascending check)
+};
+hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, int64_t ld,
+                       uint8_t* bits, int32_t* iters, int64_t batch, double* work, hipStream_t s);
+hipError_t ldpc_prepare(const LdpcGeom& g);
+size_t ldpc_work_bytes_per_frame(const LdpcGeom& g);
+
+}  // namespace pl

@@ -1,0 +1,160 @@
+// Batched LDPC flooding decoder (sum-product BP and normalised min-sum) for
+// gfx950 (MI355X).
+//
+// Semantics: src/ldpc/decoder.py of the reference --
+//   BPDecoder.decode :124-202   check update :62-96  (t = clip(tanh(m/2), +-0.999999);
+//                               leave-one-out product in ascending neighbour order,
+//                               sequential, no divide-out; clip; 2*atanh; nan_to_num),
+//                               variable update :98-122 (total = llr + np.sum(msgs));
+//                               decision total <= 0 -> 1; syndrome early stop.
+//   MSDecoder.decode :289-352   check update :257-287 (sign product * leave-one-out
+//                               min * normalization).
+// np.sum over the incoming messages is NumPy's pairwise_sum (sequential below 8
+// terms, 8 accumulators up to 128); reproduced exactly.
+//
+// Mapping (DESIGN.md §LDPC kernel): one workgroup decodes one frame; messages
+// are stored as c2v[E] plus total[n] (v2c = total - c2v, exactly how the
+// reference forms it), so the check phase, the leave-one-out phase and the
+// variable phase are each one pass over edges / variables in LDS (or in the
+// global workspace for codes whose state does not fit LDS).  Edges are laid out
+// check-major (CSR of H) so a check's inputs are contiguous.
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace pl {
+
+PL_DEV double clip999(double x) {
+    const double c = 0.999999;
+    return x < -c ? -c : (x > c ? c : x);
+}
+
+// numpy add.reduce (pairwise_sum) over msgs gathered through var_edge.
+PL_DEV double np_sum_gather(const double* C, const int32_t* __restrict__ ve, int dv) {
+    if (dv < 8) {
+        double res = 0.;
+        for (int k = 0; k < dv; ++k) res += C[ve[k]];
+        return res;
+    }
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = C[ve[j]];
+    int i = 8;
+    for (; i < dv - (dv % 8); i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += C[ve[i + j]];
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < dv; ++i) res += C[ve[i]];
+    return res;
+}
+
+template <int ALGO, bool GLOBAL>
+__global__ void __launch_bounds__(1024)
+ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
+                   uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch,
+                   double* __restrict__ work) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int64_t frame = blockIdx.x;
+    if (frame >= batch) return;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int E = g.E, n = g.n, m = g.m;
+    double* T;
+    if constexpr (GLOBAL) T = work + (int64_t)blockIdx.x * (2 * (int64_t)E + n);
+    else T = reinterpret_cast<double*>(smem);
+    double* C = T + E;
+    double* tot = C + E;
+    uint8_t* bt = GLOBAL ? smem : reinterpret_cast<uint8_t*>(tot + n);
+    const double* __restrict__ ch = llr + frame * ld;
+
+    for (int e = tid; e < E; e += nt) C[e] = 0.0;
+    for (int v = tid; v < n; v += nt) tot[v] = ch[v];  // decoder.py:144-146 (v2c = llr)
+    __syncthreads();
+    int done = g.max_iter;
+    for (int it = 0; it < g.max_iter; ++it) {
+        // check inputs v2c = total - c2v
+        for (int e = tid; e < E; e += nt) {
+            const double x = tot[dv.col_idx[e]] - C[e];
+            T[e] = (ALGO == 0) ? clip999(tanh(x / 2.0)) : x;
+        }
+        __syncthreads();
+        // leave-one-out check outputs
+        for (int e = tid; e < E; e += nt) {
+            const int c = dv.edge_chk[e];
+            const int e0 = dv.row_ptr[c], d = dv.row_ptr[c + 1] - e0, i = e - e0;
+            double o;
+            if (ALGO == 0) {
+                double p = 1.0;
+                for (int k = 0; k < d; ++k)
+                    if (k != i) p *= T[e0 + k];
+                p = clip999(p);
+                o = 2.0 * atanh(p);
+                if (isnan(o)) o = 0.0;
+                else if (isinf(o)) o = o > 0.0 ? 20.0 : -20.0;
+            } else {
+                double sp = 1.0, mn = 0.0;
+                bool first = true;
+                for (int k = 0; k < d; ++k) {
+                    if (k == i) continue;
+                    const double x = T[e0 + k];
+                    sp *= np_sign(x);
+                    const double ax = fabs(x);
+                    if (first) { mn = ax; first = false; }
+                    else if (isnan(ax) || isnan(mn)) mn = __builtin_nan("");
+                    else if (ax < mn) mn = ax;
+                }
+                o = sp * mn * g.norm;
+            }
+            C[e] = o;
+        }
+        __syncthreads();
+        // variable update + hard decision (decoder.py:171-191)
+        for (int v = tid; v < n; v += nt) {
+            const int a0 = dv.var_ptr[v], d = dv.var_ptr[v + 1] - a0;
+            const double total = ch[v] + np_sum_gather(C, dv.var_edge + a0, d);
+            tot[v] = total;
+            bt[v] = total <= 0.0 ? 1 : 0;
+        }
+        if (g.early_stop) {  // decoder.py:194-198
+            __syncthreads();
+            int bad = 0;
+            for (int c = tid; c < m; c += nt) {
+                int s = 0;
+                for (int e = dv.row_ptr[c]; e < dv.row_ptr[c + 1]; ++e) s ^= bt[dv.col_idx[e]];
+                bad |= s;
+            }
+            if (!__syncthreads_or(bad)) { done = it + 1; break; }
+        } else {
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    uint8_t* o = bits + frame * (int64_t)n;
+    for (int v = tid; v < n; v += nt) o[v] = bt[v];
+    if (iters && tid == 0) iters[frame] = done;
+}
+
+size_t ldpc_work_bytes_per_frame(const LdpcGeom& g) {
+    return g.use_global ? (size_t)(2 * (size_t)g.E + g.n) * sizeof(double) : 0;
+}
+
+template <int ALGO>
+static void* pick(bool global) {
+    return global ? (void*)ldpc_decode_kernel<ALGO, true> : (void*)ldpc_decode_kernel<ALGO, false>;
+}
+
+hipError_t ldpc_prepare(const LdpcGeom& g) {
+    void* k = g.algo == 0 ? pick<0>(g.use_global) : pick<1>(g.use_global);
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds_bytes);
+}
+
+hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, int64_t ld,
+                       uint8_t* bits, int32_t* iters, int64_t batch, double* work, hipStream_t s) {
+    void* k = g.algo == 0 ? pick<0>(g.use_global) : pick<1>(g.use_global);
+    LdpcGeom gg = g;
+    LdpcDev dd = d;
+    void* args[] = {&gg, &dd, (void*)&llr, (void*)&ld, (void*)&bits, (void*)&iters, (void*)&batch,
+                    (void*)&work};
+    return hipLaunchKernel(k, dim3((unsigned)batch), dim3(g.threads), args, g.lds_bytes, s);
+}
+
+}  // namespace pl

@@ -1,0 +1,111 @@
+"""LDPC encoder with the reference's API and outputs (src/ldpc/encoder.py:12-211).
+
+Host side (it produces frames; it is not on the decode hot path).  The
+reference's fallback for rank-deficient H, `_encode_direct` + `_solve_gf2`
+(:97-187): Gaussian elimination picks its pivots from H2 alone, so all
+right-hand sides share one elimination.
+It is evaluated here for whole batches of messages at once (one elimination,
+vectorised back-substitution) -- giving exactly the reference's
+codewords, including the *invalid* ones it emits for the seed-42 (504, 252) H
+(SURVEY.md §0 quirk 2), which is what benchmarks/throughput_test.py decodes.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+
+from .matrix import generate_ldpc_matrix
+
+
+def _systematic_generator(H: np.ndarray):
+    """(G, P) or (None, None): src/ldpc/matrix.py:135-187 (GF(2) elimination on
+    the last m columns)."""
+    m, n = H.shape
+    k = n - m
+    W = (np.asarray(H) % 2).astype(np.uint8)
+    for i in range(m):
+        col = n - m + i
+        nz = np.nonzero(W[i:, col])[0]
+        if len(nz) == 0:
+            return None, None
+        p = i + nz[0]
+        if p != i:
+            W[[i, p]] = W[[p, i]]
+        rows = np.nonzero(W[:, col])[0]
+        rows = rows[rows != i]
+        W[rows] ^= W[i]
+    P = W[:, :k].astype(int)
+    return np.hstack([np.eye(k, dtype=int), P.T]), P
+
+
+def _solve_gf2_batch(A: np.ndarray, B: np.ndarray) -> np.ndarray:
+    """The reference's _solve_gf2 (encoder.py:133-187) for many right-hand sides
+    at once: A [m, n], B [m, r] -> X [n, r]."""
+    m, n = A.shape
+    aug = np.hstack([A.astype(np.uint8) & 1, B.astype(np.uint8) & 1])
+    pivot_row = 0
+    for col in range(n):
+        if pivot_row >= m:
+            break
+        nz = np.nonzero(aug[pivot_row:, col])[0]
+        if len(nz) == 0:
+            continue
+        p = pivot_row + nz[0]
+        if p != pivot_row:
+            aug[[pivot_row, p]] = aug[[p, pivot_row]]
+        rows = np.nonzero(aug[:, col])[0]
+        rows = rows[rows != pivot_row]
+        aug[rows] ^= aug[pivot_row]
+        pivot_row += 1
+    # back-substitution exactly as the reference: x[i] = b ^ np.sum(a & x) with an
+    # integer (not mod-2) sum, so x may leave {0, 1} (then so does the codeword)
+    X = np.zeros((n, B.shape[1]), dtype=np.int64)
+    for i in range(min(pivot_row, n) - 1, -1, -1):
+        for row in range(i, m):
+            if aug[row, i] == 1 and not aug[row, :i].any():
+                X[i] = aug[row, n:].astype(np.int64) ^ (aug[row, i + 1:n, None].astype(np.int64) & X[i + 1:n]).sum(axis=0)
+                break
+    return X
+
+
+class LDPCEncoder:
+    def __init__(self, n: int, k: int, H: Optional[np.ndarray] = None, G: Optional[np.ndarray] = None,
+                 dv: int = 3, dc: int = 6, seed: Optional[int] = None):
+        assert n > k > 0, "Invalid code parameters"
+        self.n, self.k = n, k
+        if H is None:
+            self.m = n - k
+            self.H = generate_ldpc_matrix(n, k, method="mackay", dv=dv, dc=dc, seed=seed)
+        else:
+            self.H = H
+            assert H.shape[1] == n, f"H matrix must have {n} columns"
+            self.m = H.shape[0]
+        if G is not None:
+            if G.shape == (n, k):
+                self.G = G.T
+            elif G.shape == (k, n):
+                self.G = G
+            else:
+                raise ValueError(f"G shape {G.shape} doesn't match (n,k)={n,k} or (k,n)={k,n}")
+            self.P = None
+            self.use_direct_solving = False
+        else:
+            self.G, self.P = _systematic_generator(self.H)
+            self.use_direct_solving = self.G is None
+
+    def encode(self, message: np.ndarray) -> np.ndarray:
+        assert len(message) == self.k, f"Message length must be {self.k}"
+        return self.encode_batch(np.asarray(message)[None, :])[0]
+
+    def encode_batch(self, messages: np.ndarray) -> np.ndarray:
+        msg = np.asarray(messages, dtype=np.int64) & 1
+        if not self.use_direct_solving:
+            return (msg @ self.G) % 2
+        # _encode_direct (encoder.py:97-131): syndrome = H1 m mod 2, H2 p = syndrome
+        syn = (msg @ (np.asarray(self.H[:, :self.k]).T)) % 2
+        parity = _solve_gf2_batch(np.asarray(self.H[:, self.k:]), syn.T.astype(np.uint8)).T
+        return np.hstack([msg, parity]).astype(int)
+
+    def verify_codeword(self, codeword: np.ndarray) -> bool:
+        return bool(np.all((self.H @ codeword) % 2 == 0))

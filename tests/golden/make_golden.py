@@ -1,0 +1,386 @@
+#!/usr/bin/env python3
+"""Generate the golden parity fixtures under tests/golden/ from the reference.
+
+This script is the ONLY place the reference implementation is executed.  It
+runs in the build container (where /root/reference exists), imports the
+reference read-only (``sys.path.insert(0, <ref>/src)``), feeds it inputs and
+stores *data* (inputs + the reference's outputs) as small .npz files.  The
+reference never travels to the GPU box; only these vectors do.
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--ref /root/reference]
+
+Fixture inventory:
+  polar_p1.npz         F1  N=256 K=128 SC, 100 frames produced exactly in the
+                           order of benchmarks/throughput_test.py:196-228
+                           (AWGNChannel(3.0, seed=42), 10 warm-up frames first);
+                           plus SCL L=1/2/4/8 on the first 32 frames.
+  polar_sc_1024.npz    F2  SC N=1024 K=512, default + bit-reversed
+                           Bhattacharyya(2 dB) frozen sets, 0/1/3 dB.
+  polar_scl_1024_l8.npz F3 SCL N=1024 K=512 L=8 (bit-reversed Bhattacharyya)
+                           at 0/1.5/3 dB, and the default set at 3 dB.
+  polar_scl_1024_l32.npz F4 SCL N=1024 K=512 L=32.
+  polar_scl_4096_l8.npz  F5 SCL N=4096 K=2048 L=8.
+  polar_small.npz      SC/SCL over small N, odd list sizes (3, 5, 6), K
+                           extremes (1, N-1) and LLR vectors with exact zeros.
+  polar_kat16.npz      F8  docs/SCL_DECODER_README.md:115-128 KAT.
+  ldpc_bp_504.npz      F6  BP on the seed-42 mackay (504,252) H: the
+                           throughput_test.py:285-315 frames (invalid
+                           codewords, always 20 iterations) + all-zero
+                           codewords at -1/0.5/1/3 dB, with iteration counts.
+  ldpc_ms_504.npz      F7  MS (norm 1.0 and 0.75) on a (504,252) H whose row
+                           degrees are all >= 2, + BP on the same H.
+  ldpc_ms_8192.npz     F7  MS-20 on an n=8192 (3,6)-regular H.
+  crc.npz              F9  crc_encode vectors for CRC-8/16/24.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+from multiprocessing import Pool
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+
+
+def _imp():
+    sys.dont_write_bytecode = True
+    if os.path.join(REF, "src") not in sys.path:
+        sys.path.insert(0, os.path.join(REF, "src"))
+    import polar, ldpc, channel  # noqa: F401
+    return polar, ldpc, channel
+
+
+def bitrev(i, n):
+    r = 0
+    for _ in range(n):
+        r = (r << 1) | (i & 1)
+        i >>= 1
+    return r
+
+
+def bitrev_bhatta_frozen(N, K, snr=2.0):
+    polar, _, _ = _imp()
+    n = int(np.log2(N))
+    frozen, info = polar.construct_polar_code(N, K, "bhattacharyya", snr)
+    fr = np.sort(np.array([bitrev(int(i), n) for i in frozen], dtype=np.int64))
+    return fr
+
+
+def csr_from_dense(H):
+    m, n = H.shape
+    row_ptr = [0]
+    col = []
+    for i in range(m):
+        nz = np.nonzero(H[i])[0]
+        col.extend(nz.tolist())
+        row_ptr.append(len(col))
+    return np.array(row_ptr, np.int32), np.array(col, np.int32)
+
+
+def regular_36_H(n, seed):
+    """(3,6)-regular H by a seeded socket permutation; no repeated edges.
+    Every row has degree exactly 6 (so Min-Sum is defined on every check)."""
+    m = n // 2
+    rng = np.random.RandomState(seed)
+    while True:
+        sockets = np.repeat(np.arange(m), 6)
+        rng.shuffle(sockets)
+        cols = sockets.reshape(n, 3)
+        if all(len(set(r)) == 3 for r in cols):
+            H = np.zeros((m, n), dtype=np.int64)
+            for v in range(n):
+                H[cols[v], v] = 1
+            return H
+
+
+# --------------------------------------------------------------------------
+def job_p1():
+    polar, ldpc, channel = _imp()
+    N, K = 256, 128
+    enc = polar.PolarEncoder(N, K)
+    dec = polar.SCDecoder(N, K, frozen_bits=enc.get_frozen_bits_positions())
+    ch = channel.AWGNChannel(snr_db=3.0, seed=42)
+    for _ in range(10):
+        msg = np.random.randint(0, 2, K)
+        cw = enc.encode(msg)
+        llr = ch.transmit(cw, return_llr=True)
+        dec.decode(llr)
+    messages = [np.random.randint(0, 2, K) for _ in range(100)]
+    llrs = []
+    for msg in messages:
+        llrs.append(ch.transmit(enc.encode(msg), return_llr=True))
+    llrs = np.array(llrs)
+    sc = np.array([dec.decode(l) for l in llrs])
+    out = dict(N=N, K=K, frozen=np.asarray(enc.get_frozen_bits_positions(), np.int64),
+               llr=llrs, msg=np.array(messages), sc=sc)
+    for L in (1, 2, 4, 8):
+        d = polar.SCLDecoder(N, K, list_size=L, frozen_bits=enc.get_frozen_bits_positions())
+        out["scl_L%d" % L] = np.array([d.decode(l.copy()) for l in llrs[:32]])
+    return "polar_p1.npz", out
+
+
+def _polar_frames(N, K, frozen, snrs, frames, seed):
+    polar, _, channel = _imp()
+    enc = polar.PolarEncoder(N, K, frozen_bits=frozen)
+    np.random.seed(seed)
+    llr, msg, snr_col = [], [], []
+    for s in snrs:
+        ch = channel.AWGNChannel(snr_db=s)
+        for _ in range(frames):
+            m = np.random.randint(0, 2, K)
+            llr.append(ch.transmit(enc.encode(m), return_llr=True))
+            msg.append(m)
+            snr_col.append(s)
+    return np.array(llr), np.array(msg), np.array(snr_col)
+
+
+def job_sc1024():
+    polar, _, _ = _imp()
+    N, K = 1024, 512
+    out = dict(N=N, K=K)
+    default_frozen, _ = polar.generate_frozen_bits(N, K)
+    for tag, fr in (("default", np.asarray(default_frozen, np.int64)),
+                    ("bhatta", bitrev_bhatta_frozen(N, K))):
+        llr, msg, snr = _polar_frames(N, K, fr, (0.0, 1.0, 3.0), 24, 1000 + len(tag))
+        dec = polar.SCDecoder(N, K, frozen_bits=fr)
+        out[tag + "_frozen"] = fr
+        out[tag + "_llr"] = llr
+        out[tag + "_msg"] = msg
+        out[tag + "_snr"] = snr
+        out[tag + "_sc"] = np.array([dec.decode(l) for l in llr])
+    return "polar_sc_1024.npz", out
+
+
+def job_scl(N, K, L, snrs, frames, seed, name, frozen_kind="bhatta"):
+    polar, _, _ = _imp()
+    if frozen_kind == "bhatta":
+        fr = bitrev_bhatta_frozen(N, K)
+    else:
+        fr = np.asarray(polar.generate_frozen_bits(N, K)[0], np.int64)
+    llr, msg, snr = _polar_frames(N, K, fr, snrs, frames, seed)
+    dec = polar.SCLDecoder(N, K, list_size=L, frozen_bits=fr)
+    t = time.time()
+    out_bits = np.array([dec.decode(l.copy()) for l in llr])
+    dt = (time.time() - t) / len(llr)
+    return name, dict(N=N, K=K, L=L, frozen=fr, llr=llr, msg=msg, snr=snr,
+                      scl=out_bits, ref_s_per_frame=dt)
+
+
+def job_scl1024_l8():
+    a = job_scl(1024, 512, 8, (0.0, 1.5, 3.0), 20, 7, "x")[1]
+    b = job_scl(1024, 512, 8, (3.0,), 12, 8, "x", frozen_kind="default")[1]
+    out = {k: v for k, v in a.items()}
+    for k in ("frozen", "llr", "msg", "snr", "scl"):
+        out["default_" + k] = b[k]
+    return "polar_scl_1024_l8.npz", out
+
+
+def job_scl1024_l32():
+    return job_scl(1024, 512, 32, (1.0, 2.5), 4, 9, "polar_scl_1024_l32.npz")
+
+
+def job_scl4096_l8():
+    return job_scl(4096, 2048, 8, (1.5,), 3, 10, "polar_scl_4096_l8.npz")
+
+
+def job_small():
+    """Small N, odd list sizes, K extremes, zero LLRs (deterministic cases)."""
+    polar, _, channel = _imp()
+    cases = []
+    np.random.seed(77)
+    specs = [(8, 4), (16, 8), (32, 16), (64, 32), (128, 64), (64, 1), (64, 63),
+             (128, 100), (32, 5), (256, 77)]
+    for (N, K) in specs:
+        for fk in ("default", "bhatta"):
+            if fk == "default":
+                fr = np.asarray(polar.generate_frozen_bits(N, K)[0], np.int64)
+            else:
+                fr = bitrev_bhatta_frozen(N, K, 1.0)
+            enc = polar.PolarEncoder(N, K, frozen_bits=fr)
+            llrs = []
+            for snr in (0.0, 2.0):
+                ch = channel.AWGNChannel(snr_db=snr)
+                for _ in range(6):
+                    llrs.append(ch.transmit(enc.encode(np.random.randint(0, 2, K)), return_llr=True))
+            # exact zeros, tiny values and big magnitudes
+            z = llrs[0].copy(); z[::3] = 0.0
+            llrs.append(z)
+            z = llrs[1].copy(); z[1::2] = -0.0
+            llrs.append(z)
+            llrs.append(np.zeros(N))
+            t = llrs[2].copy(); t[::2] *= 1e-300
+            llrs.append(t)
+            llrs.append(llrs[3] * 1e3)
+            llrs = np.array(llrs)
+            rec = dict(N=N, K=K, frozen=fr, llr=llrs)
+            rec["sc"] = np.array([polar.SCDecoder(N, K, frozen_bits=fr).decode(l) for l in llrs])
+            for L in (1, 2, 3, 4, 5, 6, 8, 16):
+                d = polar.SCLDecoder(N, K, list_size=L, frozen_bits=fr)
+                rec["scl_L%d" % L] = np.array([d.decode(l.copy()) for l in llrs])
+            cases.append(rec)
+    out = {}
+    for ci, rec in enumerate(cases):
+        for k, v in rec.items():
+            out["c%d_%s" % (ci, k)] = v
+    out["ncases"] = len(cases)
+    return "polar_small.npz", out
+
+
+def job_kat16():
+    polar, _, channel = _imp()
+    N, K = 16, 8
+    enc = polar.PolarEncoder(N, K)
+    np.random.seed(42)
+    message = np.random.randint(0, 2, K)
+    codeword = enc.encode(message)
+    ch = channel.AWGNChannel(2.0)
+    llr = ch.transmit(codeword, return_llr=True)
+    out = dict(N=N, K=K, frozen=np.asarray(enc.frozen_bits, np.int64), msg=message,
+               codeword=codeword, llr=llr)
+    for L in (1, 2, 4, 8):
+        out["scl_L%d" % L] = polar.SCLDecoder(N, K, list_size=L, frozen_bits=enc.frozen_bits).decode(llr)
+    out["sc"] = polar.SCDecoder(N, K, frozen_bits=enc.frozen_bits).decode(llr)
+    return "polar_kat16.npz", out
+
+
+def job_bp504():
+    _, ldpc, channel = _imp()
+    n, k = 504, 252
+    enc = ldpc.LDPCEncoder(n, k, dv=3, dc=6, seed=42)
+    dec = ldpc.BPDecoder(enc.H, max_iter=20)
+    ch = channel.AWGNChannel(snr_db=3.0, seed=42)
+    for _ in range(10):
+        msg = np.random.randint(0, 2, k)
+        dec.decode(ch.transmit(enc.encode(msg), return_llr=True))
+    messages = [np.random.randint(0, 2, k) for _ in range(100)]
+    cws = [enc.encode(m) for m in messages[:24]]
+    llrs = np.array([ch.transmit(c, return_llr=True) for c in cws])
+    rp, ci = csr_from_dense(enc.H)
+    out = dict(m=enc.H.shape[0], n=n, k=k, row_ptr=rp, col_idx=ci,
+               harness_llr=llrs, harness_msg=np.array(messages[:24]), harness_cw=np.array(cws))
+    np.random.seed(99)
+    extra = np.random.randint(0, 2, (64, k))
+    out["enc_msg"] = extra
+    out["enc_cw"] = np.array([enc.encode(m) for m in extra])
+    bits, its = zip(*[dec.decode(l, return_iterations=True) for l in llrs])
+    out["harness_bits"] = np.array(bits)
+    out["harness_iters"] = np.array(its)
+    # all-zero codeword at several SNRs
+    np.random.seed(4242)
+    zl, zs = [], []
+    for s in (-1.0, 0.5, 1.0, 3.0):
+        c = channel.AWGNChannel(snr_db=s)
+        for _ in range(12):
+            zl.append(c.transmit(np.zeros(n, dtype=int), return_llr=True))
+            zs.append(s)
+    zl = np.array(zl)
+    out["zero_llr"] = zl
+    out["zero_snr"] = np.array(zs)
+    bits, its = zip(*[dec.decode(l, return_iterations=True) for l in zl])
+    out["zero_bits"] = np.array(bits)
+    out["zero_iters"] = np.array(its)
+    # no early stop, max_iter=5; and max_iter=50 with early stop
+    d2 = ldpc.BPDecoder(enc.H, max_iter=5, early_stop=False)
+    out["noes5_bits"] = np.array([d2.decode(l) for l in zl[:24]])
+    d3 = ldpc.BPDecoder(enc.H, max_iter=50, early_stop=True)
+    b3, i3 = zip(*[d3.decode(l, return_iterations=True) for l in zl[:12]])
+    out["es50_bits"] = np.array(b3)
+    out["es50_iters"] = np.array(i3)
+    return "ldpc_bp_504.npz", out
+
+
+def job_ms504():
+    _, ldpc, channel = _imp()
+    n = 504
+    H = regular_36_H(n, 5)
+    rp, ci = csr_from_dense(H)
+    np.random.seed(555)
+    llr, snr = [], []
+    for s in (0.0, 1.0, 2.0):
+        c = channel.AWGNChannel(snr_db=s)
+        for _ in range(10):
+            llr.append(c.transmit(np.zeros(n, dtype=int), return_llr=True))
+            snr.append(s)
+    llr = np.array(llr)
+    out = dict(m=H.shape[0], n=n, row_ptr=rp, col_idx=ci, llr=llr, snr=np.array(snr))
+    for norm in (1.0, 0.75):
+        d = ldpc.MSDecoder(H, max_iter=20, normalization=norm)
+        out["ms_%g" % norm] = np.array([d.decode(l) for l in llr])
+    d = ldpc.MSDecoder(H, max_iter=7, normalization=0.75, early_stop=False)
+    out["ms_noes7"] = np.array([d.decode(l) for l in llr[:10]])
+    d = ldpc.BPDecoder(H, max_iter=20)
+    b, i = zip(*[d.decode(l, return_iterations=True) for l in llr])
+    out["bp_bits"] = np.array(b)
+    out["bp_iters"] = np.array(i)
+    return "ldpc_ms_504.npz", out
+
+
+def job_ms8192():
+    _, ldpc, channel = _imp()
+    n = 8192
+    H = regular_36_H(n, 11)
+    rp, ci = csr_from_dense(H)
+    np.random.seed(8192)
+    llr = []
+    for s in (1.0, 1.5):
+        c = channel.AWGNChannel(snr_db=s)
+        for _ in range(3):
+            llr.append(c.transmit(np.zeros(n, dtype=int), return_llr=True))
+    llr = np.array(llr)
+    d = ldpc.MSDecoder(H, max_iter=20, normalization=0.75)
+    t = time.time()
+    bits = np.array([d.decode(l) for l in llr])
+    return "ldpc_ms_8192.npz", dict(m=H.shape[0], n=n, row_ptr=rp, col_idx=ci, llr=llr,
+                                    ms_0_75=bits, ref_s_per_frame=(time.time() - t) / len(llr))
+
+
+def job_crc():
+    polar, _, _ = _imp()
+    np.random.seed(31)
+    out = {}
+    for poly in ("CRC-8", "CRC-16", "CRC-24"):
+        data = np.random.randint(0, 2, (16, 40))
+        enc = np.array([polar.crc_encode(d, poly) for d in data])
+        out[poly.replace("-", "") + "_data"] = data
+        out[poly.replace("-", "") + "_enc"] = enc
+        out[poly.replace("-", "") + "_check"] = np.array([polar.crc_check(e, poly) for e in enc])
+    return "crc.npz", out
+
+
+JOBS = [job_scl4096_l8, job_scl1024_l8, job_ms8192, job_scl1024_l32, job_bp504,
+        job_sc1024, job_ms504, job_small, job_p1, job_kat16, job_crc]
+
+
+def _run(fn):
+    t = time.time()
+    name, out = fn()
+    np.savez_compressed(os.path.join(HERE, name), **out)
+    return name, time.time() - t
+
+
+def main():
+    global REF
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default=REF)
+    ap.add_argument("--only", default=None)
+    ap.add_argument("-j", type=int, default=6)
+    a = ap.parse_args()
+    REF = a.ref
+    jobs = [j for j in JOBS if a.only is None or j.__name__ in a.only.split(",")]
+    with Pool(a.j) as p:
+        for name, dt in p.imap_unordered(_run, jobs):
+            print("wrote %s in %.1fs" % (name, dt), flush=True)
+    meta = dict(numpy=np.__version__, python=platform.python_version(),
+                machine=platform.machine(), processor=platform.processor(),
+                generated=time.strftime("%Y-%m-%d %H:%M:%S"),
+                note="outputs produced by the reference implementation at " + REF)
+    with open(os.path.join(HERE, "META.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+"""Parity of the HIP LDPC decoders (BP, Min-Sum) against the reference's own
+outputs (golden fixtures) and the C oracle.  Bar: bit-exact hard decisions and
+identical iteration counts."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _L():
+    import polarcode_and_ldpc_amd.ldpc as L
+    return L
+
+
+def _H(d):
+    from polarcode_and_ldpc_amd.ldpc import csr_to_dense
+    return csr_to_dense(d["row_ptr"], d["col_idx"], int(d["n"]))
+
+
+def test_bp_harness_frames(gpu):
+    """BASELINE config 3 frames (throughput_test.py:285-315 condition: invalid
+    codewords, 20 iterations every frame)."""
+    d = golden("ldpc_bp_504.npz")
+    dec = _L().BPDecoder(_H(d), max_iter=20)
+    bits, its = dec.decode_batch(d["harness_llr"], return_iterations=True)
+    assert np.array_equal(bits, d["harness_bits"])
+    assert np.array_equal(its, d["harness_iters"])
+    b, i = dec.decode(d["harness_llr"][0], return_iterations=True)
+    assert np.array_equal(b, d["harness_bits"][0]) and i == d["harness_iters"][0]
+
+
+def test_bp_zero_codeword_snrs(gpu):
+    d = golden("ldpc_bp_504.npz")
+    L = _L()
+    H = _H(d)
+    bits, its = L.BPDecoder(H, max_iter=20).decode_batch(d["zero_llr"], return_iterations=True)
+    assert np.array_equal(bits, d["zero_bits"]) and np.array_equal(its, d["zero_iters"])
+    assert np.array_equal(L.BPDecoder(H, max_iter=5, early_stop=False).decode_batch(d["zero_llr"][:24]),
+                          d["noes5_bits"])
+    b, i = L.BPDecoder(H, max_iter=50).decode_batch(d["zero_llr"][:12], return_iterations=True)
+    assert np.array_equal(b, d["es50_bits"]) and np.array_equal(i, d["es50_iters"])
+
+
+def test_ms_504(gpu):
+    d = golden("ldpc_ms_504.npz")
+    L = _L()
+    H = _H(d)
+    for norm in (1.0, 0.75):
+        assert np.array_equal(L.MSDecoder(H, max_iter=20, normalization=norm).decode_batch(d["llr"]),
+                              d["ms_%g" % norm])
+    assert np.array_equal(L.MSDecoder(H, max_iter=7, normalization=0.75, early_stop=False)
+                          .decode_batch(d["llr"][:10]), d["ms_noes7"])
+    b, i = L.BPDecoder(H, max_iter=20).decode_batch(d["llr"], return_iterations=True)
+    assert np.array_equal(b, d["bp_bits"]) and np.array_equal(i, d["bp_iters"])
+
+
+def test_ms_8192_global_workspace(gpu):
+    """n=8192 state does not fit LDS: exercises the global-workspace kernel."""
+    d = golden("ldpc_ms_8192.npz")
+    dec = _L().MSDecoder(_H(d), max_iter=20, normalization=0.75)
+    assert dec.plan.info.lds_bytes < 64 * 1024
+    assert np.array_equal(dec.decode_batch(d["llr"]), d["ms_0_75"])
+
+
+def test_ms_degree1_raises_like_reference(gpu):
+    d = golden("ldpc_bp_504.npz")  # seed-42 mackay H has degree-1 checks
+    dec = _L().MSDecoder(_H(d), max_iter=20)
+    with pytest.raises(ValueError):
+        dec.decode(d["harness_llr"][0])
+
+
+@pytest.mark.parametrize("algo,norm,es", [("bp", 1.0, True), ("bp", 1.0, False), ("ms", 0.75, True),
+                                          ("ms", 1.0, False)])
+def test_vs_oracle_random(gpu, oracle, algo, norm, es):
+    L = _L()
+    H = L.regular_construction(504, 3, 6, seed=3) if algo == "ms" else L.mackay_construction(504, 252, 3, 6, 42)
+    rp, ci = L.dense_to_csr(H)
+    rng = np.random.RandomState(11)
+    B = 64
+    snr = rng.uniform(-1.0, 3.0, size=(B, 1))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+    llr = 2.0 * (1.0 + sigma * rng.randn(B, 504)) / sigma ** 2
+    llr[0, ::7] = 0.0  # exact zeros
+    want_b, want_i = oracle.ldpc_decode(rp, ci, 504, llr, algo=algo, max_iter=20, early_stop=es, norm=norm,
+                                        threads=8)
+    dec = L.BPDecoder(H, 20, es) if algo == "bp" else L.MSDecoder(H, 20, norm, es)
+    got_b, got_i = dec.decode_batch(llr, return_iterations=True)
+    assert np.array_equal(got_b, want_b)
+    if algo == "bp":
+        assert np.array_equal(got_i, want_i)
+
+
+def test_full_batch_bp_device(gpu):
+    """BASELINE config 3 size: B=65536 frames of the all-zero codeword at 3 dB
+    (device AWGN), decoded on device; a 64-frame sample matches the oracle."""
+    from oracle import oracle as O
+    L = _L()
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    H = L.mackay_construction(504, 252, 3, 6, 42)
+    rp, ci = L.dense_to_csr(H)
+    dec = L.BPDecoder(H, max_iter=20)
+    B = 65536
+    llr = AWGNChannel(3.0).llr_batch_device(None, 504, B, seed=5)
+    bits, its = dec.decode_batch(llr, return_iterations=True)
+    torch.cuda.synchronize()
+    idx = np.arange(0, B, B // 64)
+    want_b, want_i = O.ldpc_decode(rp, ci, 504, llr[idx].cpu().numpy(), max_iter=20, threads=8)
+    assert np.array_equal(bits[idx].cpu().numpy().astype(np.int64), want_b)
+    assert np.array_equal(its[idx].cpu().numpy(), want_i)

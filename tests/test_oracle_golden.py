@@ -1,0 +1,105 @@
+"""Pin the C oracle (oracle/refcpu.c) to the reference: every golden vector the
+reference produced (tests/golden/make_golden.py) must be reproduced bit-exactly.
+CPU only."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+
+def _bad(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape
+    return int((a != b).any(axis=1).sum())
+
+
+def test_p1_sc_and_scl(oracle):
+    d = golden("polar_p1.npz")
+    assert _bad(oracle.sc_decode(256, d["frozen"], d["llr"]), d["sc"]) == 0
+    for L in (1, 2, 4, 8):
+        assert _bad(oracle.scl_decode(256, L, d["frozen"], d["llr"][:32], threads=4), d["scl_L%d" % L]) == 0
+
+
+def test_sc_1024(oracle):
+    d = golden("polar_sc_1024.npz")
+    for tag in ("default", "bhatta"):
+        assert _bad(oracle.sc_decode(1024, d[tag + "_frozen"], d[tag + "_llr"], threads=4), d[tag + "_sc"]) == 0
+
+
+def test_scl_1024_l8(oracle):
+    d = golden("polar_scl_1024_l8.npz")
+    assert _bad(oracle.scl_decode(1024, 8, d["frozen"], d["llr"], threads=8), d["scl"]) == 0
+    assert _bad(oracle.scl_decode(1024, 8, d["default_frozen"], d["default_llr"], threads=8), d["default_scl"]) == 0
+
+
+def test_scl_l32_and_n4096(oracle):
+    d = golden("polar_scl_1024_l32.npz")
+    assert _bad(oracle.scl_decode(1024, 32, d["frozen"], d["llr"], threads=8), d["scl"]) == 0
+    d = golden("polar_scl_4096_l8.npz")
+    assert _bad(oracle.scl_decode(4096, 8, d["frozen"], d["llr"], threads=8), d["scl"]) == 0
+
+
+def test_small_cases(oracle):
+    d = golden("polar_small.npz")
+    bad = []
+    for c in range(int(d["ncases"])):
+        p = "c%d_" % c
+        N, fr, llr = int(d[p + "N"]), d[p + "frozen"], d[p + "llr"]
+        if _bad(oracle.sc_decode(N, fr, llr), d[p + "sc"]):
+            bad.append((c, "sc"))
+        for L in (1, 2, 3, 4, 5, 6, 8, 16):
+            if _bad(oracle.scl_decode(N, L, fr, llr), d[p + "scl_L%d" % L]):
+                bad.append((c, L))
+    assert not bad, bad
+
+
+def test_kat16(oracle):
+    d = golden("polar_kat16.npz")
+    for L in (1, 2, 4, 8):
+        assert np.array_equal(oracle.scl_decode(16, L, d["frozen"], d["llr"])[0], d["scl_L%d" % L])
+    assert np.array_equal(oracle.sc_decode(16, d["frozen"], d["llr"])[0], d["sc"])
+
+
+def test_bp_504(oracle):
+    d = golden("ldpc_bp_504.npz")
+    rp, ci = d["row_ptr"], d["col_idx"]
+    b, i = oracle.ldpc_decode(rp, ci, 504, d["harness_llr"])
+    assert np.array_equal(b, d["harness_bits"]) and np.array_equal(i, d["harness_iters"])
+    assert (d["harness_iters"] == 20).all()  # never converges
+    b, i = oracle.ldpc_decode(rp, ci, 504, d["zero_llr"])
+    assert np.array_equal(b, d["zero_bits"]) and np.array_equal(i, d["zero_iters"])
+    b, _ = oracle.ldpc_decode(rp, ci, 504, d["zero_llr"][:24], max_iter=5, early_stop=False)
+    assert np.array_equal(b, d["noes5_bits"])
+    b, i = oracle.ldpc_decode(rp, ci, 504, d["zero_llr"][:12], max_iter=50)
+    assert np.array_equal(b, d["es50_bits"]) and np.array_equal(i, d["es50_iters"])
+
+
+def test_ms(oracle):
+    d = golden("ldpc_ms_504.npz")
+    rp, ci = d["row_ptr"], d["col_idx"]
+    for norm in (1.0, 0.75):
+        b, _ = oracle.ldpc_decode(rp, ci, 504, d["llr"], algo="ms", norm=norm)
+        assert np.array_equal(b, d["ms_%g" % norm])
+    b, _ = oracle.ldpc_decode(rp, ci, 504, d["llr"][:10], algo="ms", norm=0.75, max_iter=7, early_stop=False)
+    assert np.array_equal(b, d["ms_noes7"])
+    b, i = oracle.ldpc_decode(rp, ci, 504, d["llr"])
+    assert np.array_equal(b, d["bp_bits"]) and np.array_equal(i, d["bp_iters"])
+    d = golden("ldpc_ms_8192.npz")
+    b, _ = oracle.ldpc_decode(d["row_ptr"], d["col_idx"], 8192, d["llr"], algo="ms", norm=0.75, threads=6)
+    assert np.array_equal(b, d["ms_0_75"])
+
+
+def test_ms_degree1_raises(oracle):
+    d = golden("ldpc_bp_504.npz")
+    with pytest.raises(ValueError):
+        oracle.ldpc_decode(d["row_ptr"], d["col_idx"], 504, d["harness_llr"][:1], algo="ms")
+
+
+def test_crc(oracle):
+    d = golden("crc.npz")
+    for L, poly in ((8, 0x1D), (16, 0x1021), (24, 0x1864CFB)):
+        tag = "CRC%d" % L
+        for data, enc, ok in zip(d[tag + "_data"], d[tag + "_enc"], d[tag + "_check"]):
+            c = oracle.crc(data, L, poly)
+            assert np.array_equal(enc[len(data):], [(c >> s) & 1 for s in range(L - 1, -1, -1)])
+            assert bool(ok) and oracle.crc(enc, L, poly) == 0

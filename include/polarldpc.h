@@ -84,6 +84,13 @@ int pl_plan_get_info(const pl_plan* plan, pl_plan_info* info);
 int pl_plan_destroy(pl_plan* plan);
 const char* pl_last_error(void);
 
+/* Diagnostic: pl_decode of a polar plan through an instrumented kernel that adds
+ * per-phase s_memtime cycle totals (summed over all frames) into stamps_dev[5]:
+ * [0] LLR update, [1] path metrics, [2] list pruning/cloning, [3] partial-sum
+ * walk, [4] final selection/output.  Timing differs from pl_decode; read shares. */
+int pl_debug_polar_stamps(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
+                          unsigned long long* stamps_dev, void* stream);
+
 /* ---- Monte-Carlo frame source (replaces src/channel/awgn.py:91-112 and the
  *      message/encode loop of benchmarks/ber_simulation.py:167-177) ---------- */
 

@@ -22,7 +22,7 @@ PL_LDPC_BP, PL_LDPC_MS = 0, 1
 EXPORTS = (
     "pl_polar_plan_create", "pl_ldpc_plan_create", "pl_decode", "pl_plan_reserve", "pl_plan_get_info",
     "pl_plan_destroy", "pl_last_error", "pl_random_bits", "pl_polar_encode", "pl_awgn_llr",
-    "pl_count_errors",
+    "pl_count_errors", "pl_debug_polar_stamps",
 )
 
 
@@ -52,6 +52,7 @@ def _load():
     L.pl_polar_encode.argtypes = [P, P, I64, P, P]
     L.pl_awgn_llr.argtypes = [P, I32, I64, D, ctypes.c_uint64, I64, P, I64, P]
     L.pl_count_errors.argtypes = [P, I64, P, I64, I32, I64, P, P]
+    L.pl_debug_polar_stamps.argtypes = [P, P, I64, I64, P, P, P]
     for name in EXPORTS:
         getattr(L, name).restype = ctypes.c_int if name != "pl_last_error" else ctypes.c_char_p
     return L
@@ -121,6 +122,12 @@ class Plan:
         it = _dptr(iters) if iters is not None else None
         check(lib.pl_decode(self._h, ctypes.c_void_p(llr.data_ptr()), B, _ld(llr), _dptr(bits), it,
                             ctypes.c_void_p(_stream(stream))), "pl_decode")
+
+    def decode_stamped(self, llr: "torch.Tensor", bits: "torch.Tensor", stamps: "torch.Tensor", stream=None):
+        """Diagnostic decode accumulating per-phase cycle totals into stamps (int64 [5])."""
+        check(lib.pl_debug_polar_stamps(self._h, ctypes.c_void_p(llr.data_ptr()), llr.shape[0], _ld(llr),
+                                        _dptr(bits), _dptr(stamps), ctypes.c_void_p(_stream(stream))),
+              "pl_debug_polar_stamps")
 
     def close(self):
         if getattr(self, "_h", None):

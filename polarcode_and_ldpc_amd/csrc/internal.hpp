@@ -20,11 +20,30 @@ struct PolarGeom {
     int surv_off;              // [lcap] x 16 B survivor table
 };
 
+// Lane-per-path decoder (polar_lane.hip): one lane = one list path, 64/lcap
+// frames per wavefront; tree depths tiered over registers / LDS / workspace.
+struct LaneGeom {
+    int N, n, K, Lsz, lcap, F, B, D, Dl, cw;
+    int lds_bytes, lds_final;
+    int lds_pool[kMaxDepth + 2];   // byte offset of LDS pool depth d (Dl <= d <= D): [2^(n-d)][64] f64
+    int lds_bl[kMaxDepth + 2];     // byte offset of single-word beta depth d: [64] u32
+    int bl_words[kMaxDepth + 2];   // beta words per slot at depth d
+    int64_t ws_pool[kMaxDepth + 2];  // workspace byte offset of pool depth d (F <= d < Dl)
+    int64_t ws_bl[kMaxDepth + 2];    // workspace byte offset of multi-word beta depth d: [words][64] u32
+    int64_t ws_walk;                 // [2][cw][64] u32 walk buffers
+    int64_t ws_bytes;                // workspace bytes per wavefront
+};
+int lane_geom(int N, int K, int list_size, int F, int lds_budget, LaneGeom* g);
+hipError_t lane_prepare(const LaneGeom& g, bool sc, int* max_blocks_per_cu);
+hipError_t lane_launch(const LaneGeom& g, bool sc, const double* llr, int64_t ld, uint8_t* out,
+                       const uint32_t* frozen_dec, const int32_t* info_pos, int64_t batch, unsigned char* ws,
+                       int grid, hipStream_t s);
+
 int polar_lcap(int list_size);  // lane-group count (power of two) for a list size
 int polar_geom(int N, int K, int list_size, int F, PolarGeom* g);  // fills layout, returns lds bytes
 hipError_t polar_launch(const PolarGeom& g, bool sc, const double* llr, int64_t ld, uint8_t* out,
                         const uint32_t* frozen_dec, const int32_t* info_pos, int64_t batch,
-                        hipStream_t s);
+                        hipStream_t s, unsigned long long* stamps = nullptr);
 hipError_t polar_prepare(const PolarGeom& g, bool sc);  // raise the kernel's LDS limit
 
 hipError_t polar_encode_launch(int N, int K, const int32_t* pos2info, const uint8_t* msg,

@@ -97,7 +97,7 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
     if (p->lane) {
         int F = flags & 0xF;
         if (!F) F = env_int("PL_POLAR_FUSED", 3);
-        const int budget = env_int("PL_POLAR_LDS_BUDGET", 16 * 1024);
+        const int budget = env_int("PL_POLAR_LDS_BUDGET", 8 * 1024);
         pl::lane_geom(N, K, p->sc ? 1 : list_size, F, budget, &p->lgeo);
         p->pg.N = N; p->pg.K = K; p->pg.F = p->lgeo.F; p->pg.lds_bytes = p->lgeo.lds_bytes;
         hipError_t e;

@@ -106,6 +106,11 @@ PL_DEV void metrics(double pm, double lam, double& m0, double& m1) {
     if (WANT1) m1 = pm + ((lam >= 0.0) ? -lam - t : -t);
 }
 
+PL_DEV void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 struct Ctx {
     const LaneGeom* g;
     unsigned char* smem;
@@ -129,28 +134,36 @@ PL_DEV uint32_t* walkbuf(const Ctx& c, int par, int w) {
     return reinterpret_cast<uint32_t*>(c.ws + c.g->ws_walk) + ((size_t)par * c.g->cw + w) * 64 + c.lane;
 }
 
-// child depth cd (size S = 2^(n-cd)) from parent depth cd-1 in lane-slot ps, own slot os
+// child depth cd (size S = 2^(n-cd)) from parent depth cd-1 in lane-slot ps, own
+// slot os.  Loads of a chunk of U outputs are issued before any store, so the
+// (possibly aliasing, as far as the compiler knows) stores do not serialise them.
 template <bool PLDS, bool CLDS>
 PL_DEV void level(const Ctx& c, int cd, bool right, int ps, int bs, int os) {
     const LaneGeom& g = *c.g;
     const int S = 1 << (g.n - cd);
-    const double* P = PLDS ? reinterpret_cast<const double*>(c.smem + g.lds_pool[cd - 1]) + ps
-                           : reinterpret_cast<const double*>(c.ws + g.ws_pool[cd - 1]) + ps;
-    double* C = CLDS ? reinterpret_cast<double*>(c.smem + g.lds_pool[cd]) + os
-                     : reinterpret_cast<double*>(c.ws + g.ws_pool[cd]) + os;
-    if (!right) {
-#pragma unroll 4
-        for (int t = 0; t < S; ++t) C[t * 64] = f_ms(P[2 * t * 64], P[(2 * t + 1) * 64]);
-    } else {
-        for (int t0 = 0; t0 < S; t0 += 32) {
-            const uint32_t bw = *blw(c, cd, t0 >> 5, bs);
-            const int te = (S - t0) < 32 ? (S - t0) : 32;
-#pragma unroll 4
-            for (int k = 0; k < te; ++k) {
-                const int t = t0 + k;
-                C[t * 64] = g_op(P[2 * t * 64], P[(2 * t + 1) * 64], bw >> k);
-            }
+    const double* __restrict__ P = PLDS ? reinterpret_cast<const double*>(c.smem + g.lds_pool[cd - 1]) + ps
+                                        : reinterpret_cast<const double*>(c.ws + g.ws_pool[cd - 1]) + ps;
+    double* __restrict__ C = CLDS ? reinterpret_cast<double*>(c.smem + g.lds_pool[cd]) + os
+                                  : reinterpret_cast<double*>(c.ws + g.ws_pool[cd]) + os;
+    constexpr int U = 8;
+    if (S < U) {
+        uint32_t bw = right ? *blw(c, cd, 0, bs) : 0u;
+        for (int t = 0; t < S; ++t) {
+            const double a = P[2 * t * 64], b = P[(2 * t + 1) * 64];
+            C[t * 64] = right ? g_op(a, b, bw >> t) : f_ms(a, b);
         }
+        return;
+    }
+    for (int t0 = 0; t0 < S; t0 += U) {
+        double a[U], b[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            a[k] = P[(2 * (t0 + k)) * 64];
+            b[k] = P[(2 * (t0 + k) + 1) * 64];
+        }
+        const uint32_t bw = right ? (*blw(c, cd, t0 >> 5, bs) >> (t0 & 31)) : 0u;
+#pragma unroll
+        for (int k = 0; k < U; ++k) C[(t0 + k) * 64] = right ? g_op(a[k], b[k], bw >> k) : f_ms(a[k], b[k]);
     }
 }
 
@@ -175,7 +188,7 @@ PL_DEV double fused_top(const Ctx& c, int i, const double* __restrict__ ch, cons
         bsl[d] = c.base + row_beta(row, d);
     }
     double lam = 0.0;
-    double* C = (F < n) ? pool(c, F, 0, os) : nullptr;
+    double* __restrict__ C = (F < n) ? pool(c, F, 0, os) : nullptr;
     for (int t = 0; t < S; ++t) {
         double v[1 << F];
         const double* src = ch + ((size_t)t << F);
@@ -235,6 +248,7 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                 int src;
                 if (dstart <= D) {
                     int d;
+                    if (dstart < c.g->Dl) __syncthreads();  // workspace written by other lanes: vmcnt(0)
                     if (dstart <= F) {
                         fused_top<F>(c, i, ch, row, lane);
                         d = F;
@@ -250,6 +264,7 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                     src = c.base + row_llr(row, D);
                 }
                 double v[8];
+                if (D < c.g->Dl) __syncthreads();  // bottom node in the workspace (tiny LDS budget)
                 const double* node = pool(c, D, 0, src);
 #pragma unroll
                 for (int k = 0; k < (1 << B); ++k) v[k] = node[k * 64];
@@ -278,21 +293,44 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
             } else {
                 double m0, m1;
                 metrics<true>(pm, lam, m0, m1);
+                // rank of (slot, b) in the stable descending order of
+                // [(m0, p) for active p] + [(m1, p) for active p]; all lane fetches of
+                // a chunk are issued before use (one LDS-crossbar round trip per chunk)
+                constexpr int QC = LCAP < 8 ? LCAP : 8;
                 int r0 = 0, r1 = 0;
-                for (int q = 0; q < nact; ++q) {
-                    const double a = bperm_d(c.base + q, m0), b = bperm_d(c.base + q, m1);
-                    r0 += (a > m0) | ((a == m0) & (q < slot));
-                    r0 += (b > m0);
-                    r1 += (a >= m1);
-                    r1 += (b > m1) | ((b == m1) & (q < slot));
+                for (int q0 = 0; q0 < nact; q0 += QC) {
+                    double a[QC], b[QC];
+#pragma unroll
+                    for (int k = 0; k < QC; ++k) {
+                        a[k] = bperm_d(c.base + q0 + k, m0);
+                        b[k] = bperm_d(c.base + q0 + k, m1);
+                    }
+#pragma unroll
+                    for (int k = 0; k < QC; ++k) {
+                        const int q = q0 + k;
+                        const bool v = q < nact;
+                        r0 += v & ((a[k] > m0) | ((a[k] == m0) & (q < slot)));
+                        r0 += v & (b[k] > m0);
+                        r1 += v & (a[k] >= m1);
+                        r1 += v & ((b[k] > m1) | ((b[k] == m1) & (q < slot)));
+                    }
                 }
                 const int nsurv = (2 * nact < g.Lsz) ? 2 * nact : g.Lsz;
                 int par = 0;
                 bit = 0;
-                for (int q = 0; q < nact; ++q) {
-                    const int a = (int)bperm(c.base + q, (uint32_t)r0), b = (int)bperm(c.base + q, (uint32_t)r1);
-                    if (a == slot) { par = q; bit = 0; }
-                    if (b == slot) { par = q; bit = 1; }
+                for (int q0 = 0; q0 < nact; q0 += QC) {
+                    int a[QC], b[QC];
+#pragma unroll
+                    for (int k = 0; k < QC; ++k) {
+                        a[k] = (int)bperm(c.base + q0 + k, (uint32_t)r0);
+                        b[k] = (int)bperm(c.base + q0 + k, (uint32_t)r1);
+                    }
+#pragma unroll
+                    for (int k = 0; k < QC; ++k) {
+                        const int q = q0 + k;
+                        if (q < nact && a[k] == slot) { par = q; bit = 0; }
+                        if (q < nact && b[k] == slot) { par = q; bit = 1; }
+                    }
                 }
                 const int sl = c.base + par;
                 const double pa = bperm_d(sl, m0), pb = bperm_d(sl, m1);
@@ -326,6 +364,7 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                     else { *walkbuf(c, 0, 0) = cur; root_par = 0; }
                 } else {
                     int parity = 0;
+                    __syncthreads();  // multi-word beta words of other lanes live in the workspace
                     *walkbuf(c, 0, 0) = cur;
                     for (; k < steps; ++k) {
                         const int cwc = 1 << (k - 5);
@@ -346,7 +385,7 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                 }
                 if (dd > 0) fill_pair(row.b0, row.b1, dd, dd + 1, slot);
             }
-            __syncthreads();  // wave-level: LDS/global writes of this leaf visible to all lanes
+            wave_fence();  // LDS is in order within a wave; only stop compiler reordering
         }
 
         // ------------------------------------------------ best path, output

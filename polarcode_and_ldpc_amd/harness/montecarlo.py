@@ -1,0 +1,187 @@
+"""Monte-Carlo BER/FER engine: frames sharded over GPUs, one all-reduce per round.
+
+Semantics follow benchmarks/ber_simulation.py:132-293 of the reference:
+per SNR point, frames of random messages are encoded, sent through BPSK/AWGN
+and decoded; BER = bit errors / (frames * K), FER = frame errors / frames, and a
+point stops once `max_errors` frame errors are seen (:191-192) or `num_frames`
+frames are done (:167).  Differences, by design:
+  * frames run in rounds of `batch` frames per rank; the stop test is applied
+    after each round (the reference stops at the exact frame), so a point may
+    overshoot max_errors by less than one round -- BER/FER stay unbiased;
+  * frame f of SNR point s uses the noise/message stream (seed, s, f) (Philox on
+    the device), so results are identical for any number of GPUs;
+  * the only collective is one all-reduce (SUM) of int64[3] = {bit errors,
+    frame errors, frames} per round (RCCL over xGMI on GPUs, gloo on CPU).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import asdict, dataclass, field
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+
+def wilson_interval(errors: int, total: int, confidence: float = 0.95):
+    """(rate, lower, upper): the Wilson score interval of
+    src/utils/metrics.py:138-167 (calculate_ber_with_confidence)."""
+    if total == 0:
+        return 0.0, 0.0, 0.0
+    from statistics import NormalDist
+    z = NormalDist().inv_cdf(1 - (1 - confidence) / 2)
+    p = errors / total
+    den = 1 + z ** 2 / total
+    center = (p + z ** 2 / (2 * total)) / den
+    margin = z * math.sqrt(p * (1 - p) / total + z ** 2 / (4 * total ** 2)) / den
+    return p, max(0.0, center - margin), min(1.0, center + margin)
+
+
+def shard(total: int, rank: int, world: int):
+    """Contiguous shard [start, start+count) of `total` frames for `rank`."""
+    base, extra = divmod(total, world)
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+@dataclass
+class PointResult:
+    snr_db: float
+    frames: int
+    frame_errors: int
+    bit_errors: int
+    info_bits: int
+    ber: float = 0.0
+    fer: float = 0.0
+    ber_ci: tuple = field(default_factory=tuple)
+    fer_ci: tuple = field(default_factory=tuple)
+    rounds: int = 0
+
+    def finalize(self):
+        tb = self.frames * self.info_bits
+        self.ber, lo, hi = wilson_interval(self.bit_errors, tb)
+        self.ber_ci = (lo, hi)
+        self.fer, lo, hi = wilson_interval(self.frame_errors, self.frames)
+        self.fer_ci = (lo, hi)
+        return self
+
+    def as_dict(self):
+        return asdict(self)
+
+
+RoundFn = Callable[[int, float, int, int], np.ndarray]
+"""round_fn(snr_index, snr_db, global_frame_offset, nframes) -> int64[3] local
+counts {bit errors, frame errors, frames} for frames [offset, offset+nframes)."""
+
+
+class MonteCarlo:
+    def __init__(self, round_fn: RoundFn, info_bits: int, batch: int, group=None, device=None):
+        self.round_fn = round_fn
+        self.info_bits = info_bits
+        self.batch = int(batch)
+        self.group = group
+        self.device = device
+        import torch.distributed as dist
+        self._dist = dist if (dist.is_available() and dist.is_initialized()) else None
+        self.rank = self._dist.get_rank(group) if self._dist else 0
+        self.world = self._dist.get_world_size(group) if self._dist else 1
+
+    def _allreduce(self, counts: np.ndarray) -> np.ndarray:
+        if self.world == 1:
+            return counts
+        import torch
+        t = torch.as_tensor(counts, dtype=torch.int64, device=self.device)
+        self._dist.all_reduce(t, group=self.group)
+        return t.cpu().numpy()
+
+    def run_point(self, snr_index: int, snr_db: float, num_frames: int, max_errors: int) -> PointResult:
+        res = PointResult(snr_db=float(snr_db), frames=0, frame_errors=0, bit_errors=0, info_bits=self.info_bits)
+        done = 0
+        while done < num_frames and res.frame_errors < max_errors:
+            round_total = min(self.batch * self.world, num_frames - done)
+            start, count = shard(round_total, self.rank, self.world)
+            local = np.zeros(3, dtype=np.int64)
+            if count > 0:
+                local = np.asarray(self.round_fn(snr_index, snr_db, done + start, count), dtype=np.int64)
+            tot = self._allreduce(local)
+            res.bit_errors += int(tot[0])
+            res.frame_errors += int(tot[1])
+            res.frames += int(tot[2])
+            res.rounds += 1
+            done += round_total
+        return res.finalize()
+
+    def run(self, snr_db_range: Sequence[float], num_frames: int, max_errors: int) -> List[PointResult]:
+        return [self.run_point(i, s, num_frames, max_errors) for i, s in enumerate(snr_db_range)]
+
+
+# ---------------------------------------------------------------------------
+# GPU round functions (device-resident frame source + decode + count)
+
+def _stream_seed(seed: int, snr_index: int) -> int:
+    return (int(seed) * 0x9E3779B97F4A7C15 + (snr_index + 1) * 0xBF58476D1CE4E5B9) & (2 ** 64 - 1)
+
+
+def polar_round_fn(decoder, seed: int = 0, crc_polynomial: Optional[str] = None):
+    """Round function for a drop-in SC/SCL decoder (polar.SCDecoder/SCLDecoder).
+    Random K-bit messages (CRC appended when crc_polynomial is given, as
+    src/polar/encoder.py:74-78 does), device polar encoder, device AWGN,
+    decode, device error count over the K decoded bits."""
+    import torch
+    from .. import _native
+    from ..channel.awgn import AWGNChannel
+    N, K = decoder.N, decoder._n_info
+    bufs = {}
+
+    def fn(snr_index, snr_db, offset, nframes):
+        if bufs.get("B", 0) < nframes:
+            bufs.update(B=nframes, msg=torch.empty((nframes, K), dtype=torch.uint8, device="cuda"),
+                        cw=torch.empty((nframes, N), dtype=torch.uint8, device="cuda"),
+                        llr=torch.empty((nframes, N), dtype=torch.float64, device="cuda"),
+                        out=torch.empty((nframes, K), dtype=torch.uint8, device="cuda"))
+        msg, cw, llr, out = (bufs[k][:nframes] for k in ("msg", "cw", "llr", "out"))
+        s = _stream_seed(seed, snr_index)
+        if crc_polynomial is None:
+            _native.random_bits(s, offset, msg)
+        else:
+            from ..polar.utils import crc_encode
+            L = int(crc_polynomial.split("-")[1])
+            data = torch.empty((nframes, K - L), dtype=torch.uint8, device="cuda")
+            _native.random_bits(s, offset, data)
+            d = data.cpu().numpy()
+            msg.copy_(torch.from_numpy(np.stack([crc_encode(r, crc_polynomial) for r in d]).astype(np.uint8)))
+        _native.polar_encode(decoder.plan, msg, cw)
+        AWGNChannel(snr_db).llr_batch_device(cw, N, nframes, seed=s ^ 0xA5A5A5A5, frame_offset=offset, out=llr)
+        decoder.plan.decode(llr, out)
+        counts = torch.zeros(3, dtype=torch.int64, device="cuda")
+        _native.count_errors(msg, out, K, counts)
+        return counts.cpu().numpy()
+
+    return fn
+
+
+def ldpc_round_fn(decoder, seed: int = 0, info_bits: Optional[int] = None):
+    """Round function for BPDecoder/MSDecoder on the all-zero codeword (BP and
+    min-sum are codeword-symmetric); errors are counted over the first
+    `info_bits` positions, like ber_simulation.py:265-269 (decoded[:k])."""
+    import torch
+    from .. import _native
+    from ..channel.awgn import AWGNChannel
+    n = decoder.n
+    k = info_bits if info_bits is not None else n - decoder.m
+    bufs = {}
+
+    def fn(snr_index, snr_db, offset, nframes):
+        if bufs.get("B", 0) < nframes:
+            bufs.update(B=nframes, llr=torch.empty((nframes, n), dtype=torch.float64, device="cuda"),
+                        out=torch.empty((nframes, n), dtype=torch.uint8, device="cuda"),
+                        its=torch.empty((nframes,), dtype=torch.int32, device="cuda"),
+                        zero=torch.zeros((nframes, n), dtype=torch.uint8, device="cuda"))
+        llr, out, its, zero = (bufs[x][:nframes] for x in ("llr", "out", "its", "zero"))
+        AWGNChannel(snr_db).llr_batch_device(None, n, nframes, seed=_stream_seed(seed, snr_index),
+                                             frame_offset=offset, out=llr)
+        decoder.plan.decode(llr, out, its)
+        counts = torch.zeros(3, dtype=torch.int64, device="cuda")
+        _native.count_errors(zero, out, k, counts)
+        return counts.cpu().numpy()
+
+    return fn

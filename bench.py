@@ -80,7 +80,16 @@ def load_traffic(name):
     if not os.path.exists(p):
         return None
     try:
-        return json.load(open(p)).get(name)
+        t = json.load(open(p)).get(name)
+        return None if t is None else float(t["bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def traffic_source(name):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        return json.load(open(p))[name]["source"]
     except Exception:
         return None
 
@@ -128,8 +137,11 @@ def bench_polar(args, rank, world):
     res = dict(value=value, ms_per_step=dt / args.steps * 1e3, kernel_ms=kms, B=B,
                roofline=dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
                              frac=achieved / HBM_PEAK_GBS, traffic=load_traffic("polar_scl_1024_l8"),
+                             traffic_unit="HBM bytes per launch (2*FETCH_SIZE+WRITE_SIZE, rocprofv3 PMC)",
+                             traffic_source=traffic_source("polar_scl_1024_l8"),
                              algorithmic_bytes_per_frame=bytes_per_frame, frames_per_launch=B,
-                             kernel="polar_decode_kernel<8,false,%d>" % plan.info.fused_top,
+                             kernel="polar_lane_kernel<%d,false,%d,%d>" % (L, plan.info.fused_top,
+                                                                            min(3, 10 - plan.info.fused_top)),
                              kernel_ms=kms),
                plan=dict(lds_bytes=plan.info.lds_bytes, fused_top=plan.info.fused_top))
     c = counts.cpu().numpy()
@@ -190,6 +202,8 @@ def bench_ldpc(args, rank, world):
                mean_iterations=mean_it, vs_published=value / 7.95e-5,
                roofline=dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
                              frac=achieved / HBM_PEAK_GBS, traffic=load_traffic("ldpc_bp_504"),
+                             traffic_unit="HBM bytes per launch (2*FETCH_SIZE+WRITE_SIZE, rocprofv3 PMC)",
+                             traffic_source=traffic_source("ldpc_bp_504"),
                              algorithmic_bytes_per_frame=bpf, frames_per_launch=B, kernel_ms=kms))
     if rank == 0 and world == 1 and not args.skip_cpu:
         from oracle import oracle as O
@@ -217,8 +231,8 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--list-size", type=int, default=8)
     ap.add_argument("--snr", type=float, default=3.0)
-    ap.add_argument("--cpu-frames", type=int, default=512)
-    ap.add_argument("--cpu-frames-ldpc", type=int, default=2048)
+    ap.add_argument("--cpu-frames", type=int, default=8192)
+    ap.add_argument("--cpu-frames-ldpc", type=int, default=65536)
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--skip-ldpc", action="store_true")
     args = ap.parse_args()

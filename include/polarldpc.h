@@ -41,7 +41,7 @@ typedef struct {
     int32_t lds_bytes;  /* dynamic LDS per workgroup of the decode kernel          */
     int32_t fused_top;  /* polar: tree depths fused into the channel read (>=1)    */
     int32_t frames_per_block; /* frames one workgroup decodes                     */
-    int32_t reserved;
+    int32_t reserved;   /* polar: kernel generation (4 tree, 3 lane, 1 group)      */
 } pl_plan_info;
 
 /* Polar SC / SCL plan.
@@ -51,7 +51,10 @@ typedef struct {
  *   index set as a mask; info bits = the complement, ascending).
  *   N power of two (2..32768); K = number of unfrozen positions, 1 <= K <= N
  *   (the reference's 0 < K < N assertion, decoder.py:17-18, is made by the
- *   Python layer on its K argument, exactly as the reference does). */
+ *   Python layer on its K argument, exactly as the reference does).
+ *   flags: 0 = fastest kernel built for (N, list size).  Diagnostics: bits 0-3
+ *   force the lane kernel (polar_lane.hip) with that fused-top depth, 0x10 the
+ *   group kernel, 0x20 the lane kernel with its default depth. */
 int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_mask, int32_t list_size,
                          int32_t flags, pl_plan** out);
 

@@ -22,6 +22,8 @@ struct pl_plan {
     uint32_t* d_frozen_dec = nullptr;  // decode-order frozen bitmask [ceil(N/32)]
     int32_t* d_info_pos = nullptr;     // [K] ascending info indices
     int32_t* d_pos2info = nullptr;     // [N] index -> info rank or -1
+    bool tree = false;      // v4 compile-time-geometry kernel (polar_tree.hip)
+    pl::TreeInfo tinfo{};
     bool lane = false;      // lane-per-path kernel (polar_lane.hip)
     pl::LaneGeom lgeo{};
     int lane_grid_max = 0;  // resident wavefronts (persistent grid)
@@ -93,7 +95,41 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
     p->list_size = list_size;
     hipGetDevice(&p->device);
     const char* kern = std::getenv("PL_POLAR_KERNEL");
-    p->lane = !(kern && std::string(kern) == "group") && !(flags & 0x10);
+    const std::string kname = kern ? kern : "";
+    {
+        int lcap = 1;
+        while (lcap < (p->sc ? 1 : list_size)) lcap <<= 1;
+        p->tree = kname != "lane" && kname != "group" && !(flags & 0x3F) &&
+                  pl::tree_lookup(n, lcap, p->sc, &p->tinfo);
+    }
+    if (p->tree) {
+        hipError_t e;
+        p->pg.N = N; p->pg.K = K; p->pg.F = p->tinfo.F; p->pg.lds_bytes = p->tinfo.lds_bytes;
+        if ((e = upload(&p->d_frozen_dec, fdec)) != hipSuccess || (e = upload(&p->d_info_pos, info)) != hipSuccess ||
+            (e = upload(&p->d_pos2info, pos2info)) != hipSuccess) {
+            pl_plan_destroy(p);
+            return hipfail(e, "plan upload");
+        }
+        int per_cu = 1;
+        if ((e = pl::tree_prepare(p->tinfo, &per_cu)) != hipSuccess) {
+            pl_plan_destroy(p);
+            return hipfail(e, "tree kernel prepare");
+        }
+        hipDeviceProp_t prop;
+        int cus = 256;
+        if (hipGetDeviceProperties(&prop, p->device) == hipSuccess && prop.multiProcessorCount > 0)
+            cus = prop.multiProcessorCount;
+        p->lane_grid_max = per_cu * cus;
+        const int waves_env = env_int("PL_POLAR_WAVES", 0);
+        if (waves_env > 0) p->lane_grid_max = waves_env;
+        if ((e = hipMalloc((void**)&p->lane_ws, (size_t)p->tinfo.ws_bytes * p->lane_grid_max)) != hipSuccess) {
+            pl_plan_destroy(p);
+            return hipfail(e, "tree workspace");
+        }
+        *out = p;
+        return PL_OK;
+    }
+    p->lane = kname != "group" && !(flags & 0x10);
     if (p->lane) {
         int F = flags & 0xF;
         if (!F) F = env_int("PL_POLAR_FUSED", 3);
@@ -251,6 +287,13 @@ extern "C" int pl_decode(pl_plan* p, const double* llr, int64_t batch, int64_t l
     hipStream_t s = (hipStream_t)stream;
     if (p->kind == 0) {
         if (ld < p->pg.N) return fail(PL_EINVAL, "ld < N");
+        if (p->tree) {
+            const int64_t need = (batch + p->tinfo.fpw - 1) / p->tinfo.fpw;
+            const int grid = (int)(need < p->lane_grid_max ? need : p->lane_grid_max);
+            hipError_t e = pl::tree_launch(p->tinfo, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, p->pg.K,
+                                           p->sc ? 1 : p->list_size, p->lane_ws, grid, nullptr, s);
+            return e == hipSuccess ? PL_OK : hipfail(e, "polar decode launch");
+        }
         if (p->lane) {
             const int fpw = 64 / p->lgeo.lcap;
             const int64_t need = (batch + fpw - 1) / fpw;
@@ -283,7 +326,16 @@ extern "C" int pl_decode(pl_plan* p, const double* llr, int64_t batch, int64_t l
 extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
                                      unsigned long long* stamps_dev, void* stream) {
     if (!p || p->kind != 0 || !stamps_dev) return fail(PL_EINVAL, "polar plan and stamp buffer required");
-    if (p->lane) return fail(PL_EUNSUPPORTED, "stamps only for the group kernel (PL_POLAR_KERNEL=group)");
+    if (p->tree) {
+        if (ld < p->pg.N) return fail(PL_EINVAL, "ld < N");
+        if (batch <= 0) return PL_OK;
+        const int64_t need = (batch + p->tinfo.fpw - 1) / p->tinfo.fpw;
+        const int grid = (int)(need < p->lane_grid_max ? need : p->lane_grid_max);
+        hipError_t e = pl::tree_launch(p->tinfo, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, p->pg.K,
+                                       p->sc ? 1 : p->list_size, p->lane_ws, grid, stamps_dev, (hipStream_t)stream);
+        return e == hipSuccess ? PL_OK : hipfail(e, "polar stamps launch");
+    }
+    if (p->lane) return fail(PL_EUNSUPPORTED, "stamps only for the tree and group kernels");
     if (!p->sc && p->pg.lcap != 8) return fail(PL_EUNSUPPORTED, "stamps build only for SC and list size 5..8");
     hipError_t e = pl::polar_launch(p->pg, p->sc, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch,
                                     (hipStream_t)stream, stamps_dev);
@@ -296,8 +348,8 @@ extern "C" int pl_plan_get_info(const pl_plan* p, pl_plan_info* info) {
     if (p->kind == 0) {
         info->kind = 0; info->n_in = p->pg.N; info->n_out = p->pg.K; info->list_size = p->list_size;
         info->lds_bytes = p->pg.lds_bytes; info->fused_top = p->pg.F;
-        info->frames_per_block = p->lane ? 64 / p->lgeo.lcap : 1;
-        info->reserved = p->lane ? p->lgeo.Dl : 0;
+        info->frames_per_block = p->tree ? p->tinfo.fpw : (p->lane ? 64 / p->lgeo.lcap : 1);
+        info->reserved = p->tree ? 4 : (p->lane ? 3 : 1);  // kernel generation: 4 tree, 3 lane, 1 group
     } else {
         info->kind = 1; info->n_in = p->lg.n; info->n_out = p->lg.n; info->list_size = 0;
         info->lds_bytes = p->lg.lds_bytes; info->fused_top = 0; info->frames_per_block = 1;

@@ -32,6 +32,7 @@
 //     u = x_hat * F^{(x)n} (an involution), computed once per frame.
 #include "common.hpp"
 #include "internal.hpp"
+#include "polar_common.hpp"
 
 namespace pl {
 
@@ -70,40 +71,6 @@ PL_DEV uint64_t bperm64(int src_lane, uint64_t x) {
 }
 PL_DEV double bperm_d(int src_lane, double v) {
     return __longlong_as_double((long long)bperm64(src_lane, (uint64_t)__double_as_longlong(v)));
-}
-
-// min-sum f with the reference's value semantics (decoder.py:121-127):
-// sign(a)*sign(b)*min(|a|,|b|); zeros give a zero, NaN in either input gives NaN.
-PL_DEV double f_ms(double a, double b) {
-    const double x = fabs(a), y = fabs(b);
-    const double mn = (y < x) ? y : x;
-    const uint64_t sb = ((uint64_t)__double_as_longlong(a) ^ (uint64_t)__double_as_longlong(b)) & 0x8000000000000000ull;
-    const double r = __longlong_as_double((long long)((uint64_t)__double_as_longlong(mn) | sb));
-    return __builtin_isunordered(a, b) ? __builtin_nan("") : r;
-}
-// g (decoder.py:129-144): btm + top if bit == 0 else btm - top
-PL_DEV double g_op(double top, double btm, uint32_t bit) {
-    const uint64_t flip = (uint64_t)(bit & 1u) << 63;
-    return btm + __longlong_as_double((long long)((uint64_t)__double_as_longlong(top) ^ flip));
-}
-
-// Path-metric increments (decoder.py:374-406), see polar_list.hip history /
-// t = log1p(exp(-|lam|)) is skipped when exp(-|lam|) < 2^(e-56),
-// e = min(ilogb pm, ilogb |lam|), pm != 0: then t is below a quarter ulp of every
-// quantity it is added to and the rounded metrics are exactly pm, pm + lam,
-// pm - lam as in the reference.
-template <bool WANT1>
-PL_DEV void metrics(double pm, double lam, double& m0, double& m1) {
-    const double x = fabs(lam);
-    int e = ilogb(pm);
-    const int ex = ilogb(x);
-    e = e < ex ? e : ex;
-    e = e < -1100 ? -1100 : (e > 1100 ? 1100 : e);  // ilogb(0) = INT_MIN: keep 56 - e finite
-    const bool skip = (pm != 0.0) && (x > (double)(56 - e) * 0.6931471805599453);
-    double t = 0.0;
-    if (!skip) t = log1p(exp(-x));
-    m0 = pm + ((lam >= 0.0) ? -t : lam - t);
-    if (WANT1) m1 = pm + ((lam >= 0.0) ? -lam - t : -t);
 }
 
 PL_DEV void wave_fence() {
@@ -287,12 +254,12 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                 bit = frozen ? 0 : (lam >= 0.0 ? 0 : 1);
             } else if (frozen) {
                 double m0, m1;
-                metrics<false>(pm, lam, m0, m1);
+                path_metrics<false>(pm, lam, m0, m1);
                 if (slot < nact) pm = m0;
                 bit = 0;
             } else {
                 double m0, m1;
-                metrics<true>(pm, lam, m0, m1);
+                path_metrics<true>(pm, lam, m0, m1);
                 // rank of (slot, b) in the stable descending order of
                 // [(m0, p) for active p] + [(m1, p) for active p]; all lane fetches of
                 // a chunk are issued before use (one LDS-crossbar round trip per chunk)

@@ -176,3 +176,47 @@ def test_reference_assertions(gpu):
         P.SCLDecoder(64, 32, list_size=0)
     with pytest.raises(AssertionError):
         P.SCDecoder(64, 32).decode(np.zeros(63))
+
+
+@pytest.mark.parametrize("snr", [0.0, 1.5, 3.0])
+def test_tree_kernel_matches_lane_kernel(gpu, oracle, snr):
+    """The v4 tree kernel (default for N=1024 L=8) against the lane kernel
+    (flags=0x20) on 4096 noisy frames, and a sample against the oracle."""
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    P = _P()
+    N, K, L, B = 1024, 512, 8, 4096
+    fr = P.construct_frozen_set(N, K, 2.0)
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    tree = _native.polar_plan(N, K, mask, L)
+    lane = _native.polar_plan(N, K, mask, L, flags=0x20)
+    assert tree.info.reserved == 4 and lane.info.reserved == 3
+    msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    _native.random_bits(11, 0, msg)
+    cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+    _native.polar_encode(tree, msg, cw)
+    llr = AWGNChannel(snr).llr_batch_device(cw, N, B, seed=5)
+    a = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    tree.decode(llr, a)
+    lane.decode(llr, b)
+    assert torch.equal(a, b)
+    ref = oracle.scl_decode(N, L, fr, llr[:48].cpu().numpy())
+    assert _mismatch(a[:48].cpu().numpy(), ref) == 0
+
+
+def test_tree_kernel_ragged_batch(gpu):
+    """Batch sizes that leave partial frame groups and fewer waves than the
+    persistent grid: every frame matches a full-batch decode of the same rows."""
+    from polarcode_and_ldpc_amd import _native
+    P = _P()
+    d = golden("polar_scl_1024_l8.npz")
+    mask = np.zeros(1024, np.uint8)
+    mask[d["frozen"]] = 1
+    plan = _native.polar_plan(1024, 512, mask, 8)
+    llr = torch.from_numpy(d["llr"]).cuda()
+    for B in sorted({1, 3, 7, 9, llr.shape[0] - 1}):
+        out = torch.empty((B, 512), dtype=torch.uint8, device="cuda")
+        plan.decode(llr[:B], out)
+        assert _mismatch(out.cpu().numpy(), d["scl"][:B]) == 0, B

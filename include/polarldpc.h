@@ -88,9 +88,12 @@ int pl_plan_destroy(pl_plan* plan);
 const char* pl_last_error(void);
 
 /* Diagnostic: pl_decode of a polar plan through an instrumented kernel that adds
- * per-phase s_memtime cycle totals (summed over all frames) into stamps_dev[5]:
- * [0] LLR update, [1] path metrics, [2] list pruning/cloning, [3] partial-sum
- * walk, [4] final selection/output.  Timing differs from pl_decode; read shares. */
+ * per-phase s_memtime cycle totals (summed over all frames) into stamps_dev[8]:
+ * tree kernel (pl_plan_info.reserved == 4): [0] fused top, [1] workspace chains,
+ * [2] LDS chain, [3] path metrics, [4] pruning/cloning, [5] partial-sum walk,
+ * [6] final selection/output, [7] workspace fences; group kernel: [0] LLR update,
+ * [1] metrics, [2] pruning, [3] walk, [4] final.  Timing differs from pl_decode;
+ * read shares. */
 int pl_debug_polar_stamps(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
                           unsigned long long* stamps_dev, void* stream);
 

@@ -1,4 +1,4 @@
-// Batched polar SC / SCL decoder for gfx950 (MI355X) -- v4 "tree" kernel:
+// Batched polar SC / SCL decoder for gfx950 (MI355X) -- the "tree" kernel:
 // lane-per-path like polar_lane.hip, with the whole tree geometry fixed at
 // compile time (template on n = log2 N and the list capacity).
 //
@@ -10,23 +10,27 @@
 // Every LLR is the same fp64 f/g of the same operands as the reference; the
 // path-metric rule is shared with polar_lane.hip (polar_common.hpp).
 //
-// What differs from polar_lane.hip:
-//   * streaming descend: the LLR update of leaf i computes depths dstart..n in
-//     chains of up to 3-4 levels per pass over the parent array -- each parent
-//     element is loaded once and folded through the whole chain in registers,
-//     every level is stored once (for the later g of its right sibling) but the
-//     left child (f) never re-reads it.  Halves workspace reads and removes the
-//     level-by-level load->store->load latency chain;
-//   * tiers by depth, all offsets compile-time constants:
-//       depth 0        channel LLRs (global, the caller's rows),
-//       depths 1..F-1  recomputed from the channel ("fused top"),
-//       depths F..DL-1 per-wave global workspace (L2 / MALL),
-//       depths DL..n-1 LDS, depth n (the leaf LLR) a register;
-//   * pointer rows are two u64 (5-bit slot per depth) and the leaf-level left
-//     partial sum is bit 63 of the beta row, so a clone is 16 bytes;
-//   * pruning runs through LDS: lanes publish (m0, m1, rows), read their frame's
-//     metrics with 16-byte LDS broadcasts, rank, and scatter survivors to a slot
-//     table -- no cross-lane shuffles.
+// Design:
+//   * one wavefront = 64/LCAP frames, lane = one list path (LCAP lanes/frame);
+//   * streaming descend: the LLR update of leaf i is ONE pass over the parent
+//     array of depth dstart-1: each parent pair is loaded once, combined (g for
+//     the right child at dstart; f/g from the channel for the fused top) and
+//     folded down to the leaf through per-depth pending registers (binary-
+//     counter order).  Every depth is stored once, as 16-byte pairs, for the
+//     later g of its right sibling; no depth is re-read by its left child;
+//   * tiers by depth, offsets compile-time constants:
+//       depth 0        channel LLRs, staged per wave transposed [N/2][frames]
+//                      (a frame's lanes share each load: one line per load),
+//       depths 1..F-1  recomputed from the channel (fused top),
+//       depths F..DL-1 per-wave global workspace, [S/2][64 lanes] f64 pairs,
+//       depths DL..n-1 LDS, same pair-interleaved layout,
+//       depth n        a register (the leaf LLR);
+//   * partial sums (beta) of depths n-5..n live in two registers per lane, the
+//     multi-word depths 1..n-6 in the workspace behind 5-bit slot pointers, as
+//     the LLR pools.  A list clone copies 24 bytes (rows + beta registers);
+//   * pruning runs through LDS: lanes publish (m0, m1) and rows, read their
+//     frame's metrics with 16-byte broadcasts (group stride padded against bank
+//     conflicts), rank, and scatter survivors to a slot table.
 #include "common.hpp"
 #include "internal.hpp"
 #include "polar_common.hpp"
@@ -37,46 +41,69 @@ namespace {
 
 constexpr int RB = 5;  // bits per slot field of a pointer row (list capacity <= 32)
 
-template <int NL, int LCAP, int F, int DL>
+template <int NL, int LCAP_, int F_, int DL_>
 struct TG {
-    static constexpr int n = NL, N = 1 << NL, FPW = 64 / LCAP;
-    static constexpr int CW = (N / 32) < 1 ? 1 : N / 32;
-    static constexpr int BW1 = (n - 5) > 1 ? (n - 5) : 1;  // first single-word beta depth
+    static constexpr int n = NL, N = 1 << NL, LCAP = LCAP_, FPW = 64 / LCAP_, F = F_, DL = DL_;
+    static constexpr int CW = N / 32;
+    static constexpr int NB = n - 6;          // multi-word beta depths 1..NB (workspace)
+    static constexpr bool STAGE = LCAP > 1;   // stage channel rows shared by a frame's lanes
+    static_assert(n >= 7 && n <= 12, "tree kernel: 7 <= n <= 12");
     static_assert(F >= 1 && F < DL && DL <= n - 1, "tiers: 1 <= F < DL <= n-1");
-    static_assert(n <= 12, "pointer rows hold depths < 12");
-    static_assert(DL >= BW1, "LDS pool depths must have single-word partial sums");
+    static_assert(F <= 4, "fused top at most 4 levels");
     // ---- LDS (bytes)
-    static constexpr int L_LLR_BYTES = 1024 * ((1 << (n - DL)) - 1);  // pools DL..n-1, [S_d][64] f64
-    static constexpr int L_BL = L_LLR_BYTES;                           // single-word beta BW1..n-1, [64] u32
-    static constexpr int L_MET = L_BL + (n - BW1) * 256;              // [64] (m0, m1)
-    static constexpr int L_ROW = L_MET + 64 * 16;                      // [64] (lrow, brow)
-    static constexpr int L_SURV = L_ROW + 64 * 16;                     // [64] u32 survivor entries
-    static constexpr int L_FINAL = L_MET;                              // [FPW][CW] u32 (aliases pruning scratch)
+    static constexpr int L_LLR_BYTES = 1024 * ((1 << (n - DL)) - 1);  // pools DL..n-1
+    static constexpr int GS = LCAP * 16 + 16;                          // padded group stride (16-B entries)
+    static constexpr int L_MET = L_LLR_BYTES;                          // [FPW][GS]: (m0, m1)
+    static constexpr int L_ROW = L_MET + FPW * GS;                     // [FPW][GS]: (lrow, brow)
+    static constexpr int L_BR = L_ROW + FPW * GS;                      // [64] u64: beta registers
+    static constexpr int L_SURV = L_BR + 64 * 8;                       // [64] u32: survivor entries
+    static constexpr int L_FINAL = L_MET;                              // [FPW][CW] u32 (aliases scratch)
     static constexpr int L_END0 = L_SURV + 64 * 4;
     static constexpr int L_END1 = L_FINAL + FPW * CW * 4;
     static constexpr int LDS = (((L_END0 > L_END1) ? L_END0 : L_END1) + 15) & ~15;
     // ---- workspace (bytes per wave)
-    static constexpr int64_t W_LLR_BYTES = 1024LL * ((1LL << (n - F)) - (1LL << (n - DL)));  // pools F..DL-1
-    static constexpr int64_t W_BL = W_LLR_BYTES;  // multi-word beta depths 1..BW1-1, [W_d][64] u32
-    static constexpr int64_t W_BL_BYTES = 8LL * ((1LL << n) - (1LL << (n - BW1 + 1)));
+    static constexpr int64_t W_CH_BYTES = STAGE ? (int64_t)N * FPW * 8 : 0;  // [N/2][FPW] f64 pairs
+    static constexpr int64_t W_LLR = W_CH_BYTES;                               // pools F..DL-1
+    static constexpr int64_t W_LLR_BYTES = 1024LL * ((1LL << (n - F)) - (1LL << (n - DL)));
+    static constexpr int64_t W_BL = W_LLR + W_LLR_BYTES;  // beta depths 1..NB: [W_d][64] u32
+    static constexpr int64_t W_BL_BYTES = 8LL * ((1LL << n) - (1LL << (n - NB)));
     static constexpr int64_t W_WALK = W_BL + W_BL_BYTES;  // [2][CW][64] u32
     static constexpr int64_t WS = (W_WALK + 2LL * CW * 256 + 255) & ~255LL;
 
-    PL_DEV static int l_llr(int d) { return 1024 * ((1 << (n - DL)) - (1 << (n - d))); }
-    PL_DEV static int64_t w_llr(int d) { return 1024LL * ((1LL << (n - F)) - (1LL << (n - d))); }
-    PL_DEV static int l_bl(int d) { return L_BL + (d - BW1) * 256; }
-    PL_DEV static int64_t w_bl(int d) { return W_BL + 8LL * ((1LL << n) - (1LL << (n - d + 1))); }
+    // byte offset of the pool of depth d (LDS if d >= DL, else workspace);
+    // pair j of lane-slot s sits at offset + (j * 64 + s) * 16
+    static constexpr int64_t llr_off(int d) {
+        return d >= DL ? (int64_t)1024 * ((1 << (n - DL)) - (1 << (n - d)))
+                       : W_LLR + 1024LL * ((1LL << (n - F)) - (1LL << (n - d)));
+    }
+    // byte offset of the beta pool of multi-word depth d (1..NB); word w of slot s at + (w*64 + s)*4
+    static constexpr int64_t bl_off(int d) { return W_BL + 8LL * ((1LL << n) - (1LL << (n - d + 1))); }
 };
 
 PL_DEV int field(uint64_t row, int d) { return (int)((row >> (RB * d)) & 31u); }
-PL_DEV uint64_t range_mask(int lo, int hi) {  // fields [lo, hi)
-    const uint64_t h = (RB * hi >= 64) ? ~0ull : ((1ull << (RB * hi)) - 1ull);
-    const uint64_t l = (1ull << (RB * lo)) - 1ull;
-    return h & ~l;
+PL_DEV uint64_t set_field(uint64_t row, int d, int v) {
+    return (row & ~(31ull << (RB * d))) | ((uint64_t)v << (RB * d));
 }
-PL_DEV uint64_t set_range(uint64_t row, uint64_t own, int lo, int hi) {
-    const uint64_t m = range_mask(lo, hi);
+PL_DEV uint64_t set_range(uint64_t row, uint64_t own, int lo, int hi) {  // fields [lo, hi) := own
+    const uint64_t h = (RB * hi >= 64) ? ~0ull : ((1ull << (RB * hi)) - 1ull);
+    const uint64_t m = h & ~((1ull << (RB * lo)) - 1ull);
     return (row & ~m) | (own & m);
+}
+
+// Partial sums of depths n-5..n in registers: bb holds depth n-k (k = 0..4) at
+// bit offset 2^k - 1 (width 2^k); bw5 is the 32-bit word of depth n-5.
+template <int n>
+PL_DEV uint32_t beta_get(int d, uint32_t bb, uint32_t bw5) {
+    const int k = n - d;
+    if (k == 5) return bw5;
+    return (bb >> ((1 << k) - 1)) & ((1u << (1 << k)) - 1u);
+}
+template <int n>
+PL_DEV void beta_set(int d, uint32_t v, uint32_t& bb, uint32_t& bw5) {
+    const int k = n - d;
+    if (k == 5) { bw5 = v; return; }
+    const uint32_t m = ((1u << (1 << k)) - 1u) << ((1 << k) - 1);
+    bb = (bb & ~m) | ((v << ((1 << k) - 1)) & m);
 }
 
 // Global workspace written by other lanes of this wave: wait for this wave's
@@ -92,30 +119,118 @@ PL_DEV void lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// One streaming chain of C levels: parent values ld(e) at depth p; level k (1..C)
-// is depth p+k; level 1 is g (bits from bits(t), bit j = element t*2^(C-1)+j)
-// when GF, all other levels f.  st(k, idx, v) stores level k element idx, except
-// the last level when LAST (the leaf LLR, returned).
-template <int C, bool GF, bool LAST, class LD, class ST, class BT>
-PL_DEV double chain(int nout, const LD& ld, const ST& st, const BT& bits) {
-    double lam = 0.0;
-    for (int t = 0; t < nout; ++t) {
-        double v[1 << C];
+template <class G>
+struct Fold {
+    double pend[G::n + 1];  // pending even element per depth
+    double lam;             // the leaf LLR (depth n)
+};
+
+// Element idx of depth D has been computed: if even, hold it; if odd, store the
+// (even, odd) pair to this lane's slot and continue one depth down with f.
+// Compile-time recursion keeps every pending value in a register.
+template <class G, int D>
+PL_DEV void fold(Fold<G>& st, double v, int idx, unsigned char* smem, unsigned char* ws, int lane) {
+    if constexpr (D == G::n) {
+        st.lam = v;
+    } else {
+        if (idx & 1) {
+            double2* dst = reinterpret_cast<double2*>((D >= G::DL ? smem : ws) + G::llr_off(D));
+            dst[(idx >> 1) * 64 + lane] = make_double2(st.pend[D], v);
+            fold<G, D + 1>(st, f_ms(st.pend[D], v), idx >> 1, smem, ws, lane);
+        } else {
+            st.pend[D] = v;
+        }
+    }
+}
+
+// Right child at depth Q = P+1: g over the parent pairs (slot ps) with the left
+// sibling's partial sums, then the f-chain down to the leaf.
+template <class G, int P>
+PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int lane, int ps, int bs, uint32_t bb,
+                        uint32_t bw5) {
+    constexpr int n = G::n, Q = P + 1, SQ = 1 << (n - Q);
+    Fold<G> st;
+    st.lam = 0.0;
+    const double2* src = reinterpret_cast<const double2*>((P >= G::DL ? smem : ws) + G::llr_off(P)) + ps;
+    uint32_t w = 0;
+    if constexpr (Q > G::NB) w = beta_get<n>(Q, bb, bw5);
+    const uint32_t* bsrc = reinterpret_cast<const uint32_t*>(ws + G::bl_off(Q <= G::NB ? Q : 1)) + bs;
+    constexpr int U = SQ < 8 ? SQ : 8;  // parent pairs in flight
+#pragma unroll 1
+    for (int t0 = 0; t0 < SQ; t0 += U) {
+        double2 pr[U];
 #pragma unroll
-        for (int k = 0; k < (1 << C); ++k) v[k] = ld(t * (1 << C) + k);
-        const uint32_t bw = GF ? bits(t) : 0u;
+        for (int k = 0; k < U; ++k) pr[k] = src[(t0 + k) * 64];
+        if constexpr (Q <= G::NB) {
+            if ((t0 & 31) == 0) w = bsrc[(t0 >> 5) * 64];
+        }
 #pragma unroll
-        for (int lv = 1; lv <= C; ++lv) {
-            const int m = 1 << (C - lv);
+        for (int k = 0; k < U; ++k)
+            fold<G, Q>(st, g_op(pr[k].x, pr[k].y, w >> ((t0 + k) & 31)), t0 + k, smem, ws, lane);
+    }
+    return st.lam;
+}
+
+// Fused top: depth-F elements from 2^F channel values each (level d is g where
+// the depth-d ancestor of leaf i is a right child), then the f-chain to the leaf.
+template <class G>
+PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, int fw, int i, const double* ch,
+                            uint64_t brow, int base, uint32_t bb, uint32_t bw5) {
+    constexpr int n = G::n, F = G::F, SF = 1 << (n - F);
+    Fold<G> st;
+    st.lam = 0.0;
+    bool right[F + 1];
+    const uint32_t* bsrc[F + 1];
+    uint32_t bw[F + 1];
 #pragma unroll
-            for (int k = 0; k < m; ++k) {
-                v[k] = (GF && lv == 1) ? g_op(v[2 * k], v[2 * k + 1], bw >> k) : f_ms(v[2 * k], v[2 * k + 1]);
-                if (!(LAST && lv == C)) st(lv, t * m + k, v[k]);
+    for (int d = 1; d <= F; ++d) {
+        right[d] = (i >> (n - d)) & 1;
+        bsrc[d] = reinterpret_cast<const uint32_t*>(ws + G::bl_off(d <= G::NB ? d : 1)) + base + field(brow, d);
+        bw[d] = (d > G::NB) ? beta_get<n>(d, bb, bw5) : 0u;
+    }
+    const double2* chs = reinterpret_cast<const double2*>(ws) + fw;  // staged [N/2][FPW]
+#pragma unroll 2
+    for (int t = 0; t < SF; ++t) {
+        double v[1 << F];
+        if constexpr (G::STAGE) {
+#pragma unroll
+            for (int k = 0; k < (1 << (F - 1)); ++k) {
+                const double2 pr = chs[((t << (F - 1)) + k) * G::FPW];
+                v[2 * k] = pr.x;
+                v[2 * k + 1] = pr.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < (1 << F); ++k) v[k] = ch[(t << F) + k];
+        }
+#pragma unroll
+        for (int d = 1; d <= F; ++d) {
+            const int e0 = t << (F - d);  // depth-d element index of v[0]
+            const int m = 1 << (F - d);
+            if (right[d]) {
+                if (d <= G::NB && (e0 & 31) == 0) bw[d] = bsrc[d][(e0 >> 5) * 64];
+                const uint32_t b = bw[d] >> (e0 & 31);
+#pragma unroll
+                for (int k = 0; k < m; ++k) v[k] = g_op(v[2 * k], v[2 * k + 1], b >> k);
+            } else {
+#pragma unroll
+                for (int k = 0; k < m; ++k) v[k] = f_ms(v[2 * k], v[2 * k + 1]);
             }
         }
-        lam = v[0];
+        fold<G, F>(st, v[0], t, smem, ws, lane);
     }
-    return lam;
+    return st.lam;
+}
+
+template <class G, int P>
+PL_DEV double descend_from(int p, unsigned char* smem, unsigned char* ws, int lane, int ps, int bs, uint32_t bb,
+                           uint32_t bw5) {
+    if constexpr (P >= G::n) {
+        return 0.0;
+    } else {
+        if (p == P) return descend_g<G, P>(smem, ws, lane, ps, bs, bb, bw5);
+        return descend_from<G, P + 1>(p, smem, ws, lane, ps, bs, bb, bw5);
+    }
 }
 
 }  // namespace
@@ -126,7 +241,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                   const uint32_t* __restrict__ frozen_dec, const int32_t* __restrict__ info_pos, int64_t batch,
                   int K, int Lsz, unsigned char* __restrict__ workspace, unsigned long long* __restrict__ stamps) {
     using G = TG<NL, LCAP, F, DL>;
-    constexpr int n = G::n, N = G::N, FPW = G::FPW, BW1 = G::BW1;
+    constexpr int n = G::n, N = G::N, FPW = G::FPW;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
     const int fw = lane / LCAP, slot = lane % LCAP, base = fw * LCAP;
@@ -134,165 +249,84 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
     uint64_t own = 0;
 #pragma unroll
     for (int d = 0; d < 12; ++d) own |= (uint64_t)slot << (RB * d);
+    double2* const met = reinterpret_cast<double2*>(smem + G::L_MET + fw * G::GS);    // [LCAP] of this frame
+    uint64_t* const rowx = reinterpret_cast<uint64_t*>(smem + G::L_ROW + fw * G::GS);  // [LCAP][2]
+    uint64_t* const brx = reinterpret_cast<uint64_t*>(smem + G::L_BR) + base;          // [LCAP]
+    uint32_t* const surv = reinterpret_cast<uint32_t*>(smem + G::L_SURV) + base;       // [LCAP]
+    uint32_t* const walk = reinterpret_cast<uint32_t*>(ws + G::W_WALK) + lane;          // [2][CW][64]
 
-    unsigned long long acc[5] = {0, 0, 0, 0, 0};
+    unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tprev = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-#define STAMP(k)                                                   \
-    if constexpr (STAMPS) {                                        \
+#define STAMP(k)                                                    \
+    if constexpr (STAMPS) {                                         \
         const unsigned long long tn = __builtin_amdgcn_s_memtime(); \
-        acc[k] += tn - tprev;                                      \
-        tprev = tn;                                                \
+        acc[k] += tn - tprev;                                       \
+        tprev = tn;                                                 \
     }
 
     for (int64_t f0 = (int64_t)blockIdx.x * FPW; f0 < batch; f0 += (int64_t)gridDim.x * FPW) {
         const int64_t frame = f0 + fw;
         const bool live = frame < batch;
         const double* __restrict__ ch = llr + (live ? frame : batch - 1) * ld;
-        uint64_t lrow = own, brow = own & ~(1ull << 63);
+        if constexpr (G::STAGE) {
+            // channel rows of this wave's frames -> [N/2][FPW] pairs (lane: frame l%FPW)
+            const int sf = lane % FPW;
+            const int64_t fr = f0 + sf < batch ? f0 + sf : batch - 1;
+            const double* row = llr + fr * ld;
+            double2* dst = reinterpret_cast<double2*>(ws);
+            constexpr int PPI = 64 / FPW;  // pairs per frame per instruction
+#pragma unroll 4
+            for (int pb = 0; pb < N / 2; pb += PPI) {
+                const int pr = pb + lane / FPW;
+                dst[pr * FPW + sf] = make_double2(row[2 * pr], row[2 * pr + 1]);
+            }
+        }
+        uint64_t lrow = own, brow = own;
+        uint32_t bb = 0, bw5 = 0;
         double pm = (slot == 0) ? 0.0 : -INFINITY;
         int nact = 1;
         int root_par = 0;
+        STAMP(7);
 
         for (int i = 0; i < N; ++i) {
             // ================================================ LLRs down to leaf i
             const int dstart = (i == 0) ? 1 : n - __builtin_ctz(i);
             double lam;
-            {
-                int p;
-                bool gfirst;
-                if (dstart <= DL) ws_sync();  // workspace data of other lanes (pools, multi-word betas)
-                if (dstart <= F) {
-                    // ---- fused top: depth F from the channel, levels 1..F (g where the
-                    // ancestor at that depth is a right child), stored in the workspace
-                    double* __restrict__ dst = reinterpret_cast<double*>(ws + G::w_llr(F)) + lane;
-                    bool right[F + 1];
-                    const uint32_t* bsrc[F + 1];
-#pragma unroll
-                    for (int d = 1; d <= F; ++d) {
-                        right[d] = (i >> (n - d)) & 1;
-                        const int bs = base + field(brow, d);
-                        bsrc[d] = (d >= BW1) ? reinterpret_cast<const uint32_t*>(smem + G::l_bl(d)) + bs
-                                             : reinterpret_cast<const uint32_t*>(ws + G::w_bl(d)) + bs;
-                    }
-                    constexpr int SF = 1 << (n - F);
-#pragma unroll 2
-                    for (int t = 0; t < SF; ++t) {
-                        double v[1 << F];
-                        const double* src = ch + ((size_t)t << F);
-#pragma unroll
-                        for (int k = 0; k < (1 << F); ++k) v[k] = src[k];
-#pragma unroll
-                        for (int d = 1; d <= F; ++d) {
-                            const int e0 = t << (F - d);  // depth-d element index of v[0]
-                            const int m = 1 << (F - d);
-                            if (right[d]) {
-                                const uint32_t bw = bsrc[d][(d >= BW1) ? 0 : (e0 >> 5) * 64] >> (e0 & 31);
-#pragma unroll
-                                for (int k = 0; k < m; ++k) v[k] = g_op(v[2 * k], v[2 * k + 1], bw >> k);
-                            } else {
-#pragma unroll
-                                for (int k = 0; k < m; ++k) v[k] = f_ms(v[2 * k], v[2 * k + 1]);
-                            }
-                        }
-                        dst[(size_t)t * 64] = v[0];
-                    }
-                    lrow = set_range(lrow, own, F, F + 1);
-                    p = F;
-                    gfirst = false;
-                } else {
-                    p = dstart - 1;
-                    gfirst = true;
-                }
-                // ---- workspace chains: depths p+1 .. DL-1
-                while (p < DL - 1) {
-                    const int C = (DL - 1 - p) < 3 ? (DL - 1 - p) : 3;
-                    const int ps = base + (gfirst ? field(lrow, p) : slot);  // parent slot
-                    const double* P = reinterpret_cast<const double*>(ws + G::w_llr(p)) + ps;
-                    const int bsl = base + field(brow, p + 1);
-                    const int d1 = p + 1;
-                    auto ld = [&](int e) { return P[(size_t)e * 64]; };
-                    auto st = [&](int k, int idx, double v) {
-                        reinterpret_cast<double*>(ws + G::w_llr(p + k))[(size_t)idx * 64 + lane] = v;
-                    };
-                    const int nout = 1 << (n - p - C);
-                    if (gfirst) {
-                        auto bits = [&](int t) -> uint32_t {
-                            const int e0 = t << (C - 1);
-                            const uint32_t w = (d1 >= BW1)
-                                ? reinterpret_cast<const uint32_t*>(smem + G::l_bl(d1))[bsl]
-                                : reinterpret_cast<const uint32_t*>(ws + G::w_bl(d1))[(e0 >> 5) * 64 + bsl];
-                            return w >> (e0 & 31);
-                        };
-                        if (C == 3) chain<3, true, false>(nout, ld, st, bits);
-                        else if (C == 2) chain<2, true, false>(nout, ld, st, bits);
-                        else chain<1, true, false>(nout, ld, st, bits);
-                    } else {
-                        auto nb = [](int) -> uint32_t { return 0u; };
-                        if (C == 3) chain<3, false, false>(nout, ld, st, nb);
-                        else if (C == 2) chain<2, false, false>(nout, ld, st, nb);
-                        else chain<1, false, false>(nout, ld, st, nb);
-                    }
-                    lrow = set_range(lrow, own, p + 1, p + 1 + C);
-                    p += C;
-                    gfirst = false;
-                }
-                // ---- LDS chains ending at the leaf: depths p+1 .. n-1 stored, depth n returned
-                {
-                    const int C = n - p;
-                    const int ps = base + (gfirst ? field(lrow, p) : slot);
-                    const bool pws = (p < DL);
-                    const double* P = pws ? reinterpret_cast<const double*>(ws + G::w_llr(p)) + ps
-                                          : reinterpret_cast<const double*>(smem + G::l_llr(p)) + ps;
-                    const int d1 = p + 1;
-                    const int bsl = base + field(brow, d1 < n ? d1 : 0);
-                    auto st = [&](int k, int idx, double v) {
-                        reinterpret_cast<double*>(smem + G::l_llr(p + k))[idx * 64 + lane] = v;
-                    };
-                    auto bits = [&](int) -> uint32_t {
-                        if (d1 == n) return (uint32_t)(brow >> 63);
-                        return reinterpret_cast<const uint32_t*>(smem + G::l_bl(d1))[bsl];
-                    };
-                    auto nb = [](int) -> uint32_t { return 0u; };
-                    if (pws) {
-                        auto ld = [&](int e) { return P[(size_t)e * 64]; };
-                        constexpr int CC = n - DL + 1;  // p == DL-1
-                        lam = gfirst ? chain<CC, true, true>(1, ld, st, bits) : chain<CC, false, true>(1, ld, st, nb);
-                    } else {
-                        auto ld = [&](int e) { return P[e * 64]; };
-                        // from an LDS parent the chain always starts with g (dstart > DL)
-                        static_assert(n - DL <= 4, "LDS tier deeper than 4 levels");
-                        if (C == 1) lam = chain<1, true, true>(1, ld, st, bits);
-                        else if (C == 2 || n - DL < 3) lam = chain<(n - DL < 2 ? n - DL : 2), true, true>(1, ld, st, bits);
-                        else if (C == 3 || n - DL < 4) lam = chain<(n - DL < 3 ? n - DL : 3), true, true>(1, ld, st, bits);
-                        else lam = chain<4, true, true>(1, ld, st, bits);
-                    }
-                    if (C > 1) lrow = set_range(lrow, own, p + 1, n);
-                }
+            if (dstart <= DL) ws_sync();  // workspace written by other lanes
+            STAMP(7);
+            if (dstart <= F) {
+                lam = descend_fused<G>(smem, ws, lane, fw, i, ch, brow, base, bb, bw5);
+                lrow = set_range(lrow, own, F, n);
+                STAMP(0);
+            } else {
+                const int p = dstart - 1;
+                const int ps = base + field(lrow, p);
+                const int bs = base + field(brow, dstart <= G::NB ? dstart : 0);
+                lam = descend_from<G, F>(p, smem, ws, lane, ps, bs, bb, bw5);
+                lrow = set_range(lrow, own, dstart, n);
+                if (p < DL) { STAMP(1); } else { STAMP(2); }
             }
-            STAMP(0);
 
             // ================================================ decision at leaf i
             const bool frozen = (frozen_dec[i >> 5] >> (i & 31)) & 1u;
             int bit;
             if constexpr (SC) {
                 bit = frozen ? 0 : (lam >= 0.0 ? 0 : 1);
-                STAMP(1);
+                STAMP(3);
             } else if (frozen) {
                 double m0, m1;
                 path_metrics<false>(pm, lam, m0, m1);
                 if (slot < nact) pm = m0;
                 bit = 0;
-                STAMP(1);
+                STAMP(3);
             } else {
                 double m0, m1;
                 path_metrics<true>(pm, lam, m0, m1);
-                STAMP(1);
-                double2* metv = reinterpret_cast<double2*>(smem + G::L_MET);
-                uint64_t* rowv = reinterpret_cast<uint64_t*>(smem + G::L_ROW);
-                uint32_t* surv = reinterpret_cast<uint32_t*>(smem + G::L_SURV);
-                metv[lane] = make_double2(m0, m1);
-                rowv[2 * lane] = lrow;
-                rowv[2 * lane + 1] = brow;
+                STAMP(3);
+                met[slot] = make_double2(m0, m1);
+                rowx[2 * slot] = lrow;
+                rowx[2 * slot + 1] = brow;
+                brx[slot] = (uint64_t)bb | ((uint64_t)bw5 << 32);
                 lds_sync();
                 // rank of (slot, b) in the stable descending order of
                 // [(m0, q) for active q] + [(m1, q) for active q]
@@ -301,7 +335,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 for (int q0 = 0; q0 < nact; q0 += QC) {
                     double2 mq[QC];
 #pragma unroll
-                    for (int k = 0; k < QC; ++k) mq[k] = metv[base + q0 + k];
+                    for (int k = 0; k < QC; ++k) mq[k] = met[q0 + k];
 #pragma unroll
                     for (int k = 0; k < QC; ++k) {
                         const int q = q0 + k;
@@ -315,25 +349,28 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 }
                 const int nsurv = (2 * nact < Lsz) ? 2 * nact : Lsz;
                 if (slot < nact) {
-                    if (r0 < nsurv) surv[base + r0] = (uint32_t)(slot << 1);
-                    if (r1 < nsurv) surv[base + r1] = (uint32_t)((slot << 1) | 1);
+                    if (r0 < nsurv) surv[r0] = (uint32_t)(slot << 1);
+                    if (r1 < nsurv) surv[r1] = (uint32_t)((slot << 1) | 1);
                 }
                 lds_sync();
                 bit = 0;
                 if (slot < nsurv) {
-                    const uint32_t e = surv[base + slot];
-                    const int par = base + (int)(e >> 1);
+                    const uint32_t e = surv[slot];
+                    const int par = (int)(e >> 1);
                     bit = (int)(e & 1u);
-                    const double2 pmv = metv[par];
+                    const double2 pmv = met[par];
                     pm = bit ? pmv.y : pmv.x;
-                    lrow = rowv[2 * par];
-                    brow = rowv[2 * par + 1];
+                    lrow = rowx[2 * par];
+                    brow = rowx[2 * par + 1];
+                    const uint64_t br = brx[par];
+                    bb = (uint32_t)br;
+                    bw5 = (uint32_t)(br >> 32);
                 } else {
                     pm = -INFINITY;
                 }
                 nact = nsurv;
                 lds_sync();  // scratch reads done before the next leaf's writes
-                STAMP(2);
+                STAMP(4);
             }
 
             // ================================================ partial-sum walk
@@ -344,71 +381,57 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 uint32_t cur = (uint32_t)bit;
                 int k = 0;
                 for (; k < steps && k < 5; ++k) {
-                    const uint32_t left = (dd == n)
-                        ? (uint32_t)(brow >> 63)
-                        : reinterpret_cast<const uint32_t*>(smem + G::l_bl(dd))[base + field(brow, dd)];
+                    const uint32_t left = beta_get<n>(dd, bb, bw5);
                     const uint32_t msk = (1u << (1 << k)) - 1u;
                     cur = spread16((left ^ cur) & msk) | (spread16(cur & msk) << 1);
                     --dd;
                 }
-                uint32_t* walk = reinterpret_cast<uint32_t*>(ws + G::W_WALK) + lane;  // [2][CW][64]
                 if (k == steps) {
-                    if (dd == n) {
-                        brow = (brow & ~(1ull << 63)) | ((uint64_t)bit << 63);
-                    } else if (dd > 0) {
-                        reinterpret_cast<uint32_t*>(smem + G::l_bl(dd))[lane] = cur;
-                        brow = set_range(brow, own, dd, dd + 1);
-                    } else {
-                        walk[0] = cur;
-                        root_par = 0;
-                    }
+                    beta_set<n>(dd, cur, bb, bw5);  // dd >= n-5: a left child, kept in registers
                 } else {
+                    // dd == n-5, cur = one word: multi-word combine through the workspace
                     int parity = 0;
                     ws_sync();  // multi-word betas of other lanes live in the workspace
                     walk[0] = cur;
                     for (; k < steps; ++k) {
                         const int cwc = 1 << (k - 5);
-                        const int ls = base + field(brow, dd);
+                        const int ls = base + field(brow, dd <= G::NB ? dd : 0);
                         const bool last = (k + 1 == steps);
+                        const uint32_t* lsrc = reinterpret_cast<const uint32_t*>(ws + G::bl_off(dd <= G::NB ? dd : 1)) + ls;
+                        uint32_t* ldst = reinterpret_cast<uint32_t*>(ws + G::bl_off(dd - 1 >= 1 ? dd - 1 : 1)) + lane;
                         for (int w = 0; w < 2 * cwc; ++w) {
                             const uint32_t cwv = walk[(parity * G::CW + (w >> 1)) * 64];
-                            const uint32_t lw = (dd >= BW1)
-                                ? reinterpret_cast<const uint32_t*>(smem + G::l_bl(dd))[ls]
-                                : reinterpret_cast<const uint32_t*>(ws + G::w_bl(dd))[(w >> 1) * 64 + ls];
+                            const uint32_t lw = (dd > G::NB) ? bw5 : lsrc[(w >> 1) * 64];
                             const int sh = (w & 1) * 16;
                             const uint32_t r = spread16((lw ^ cwv) >> sh) | (spread16(cwv >> sh) << 1);
-                            if (last && dd - 1 > 0)
-                                reinterpret_cast<uint32_t*>(ws + G::w_bl(dd - 1))[w * 64 + lane] = r;
-                            else
-                                walk[((parity ^ 1) * G::CW + w) * 64] = r;
+                            if (last && dd - 1 > 0) ldst[w * 64] = r;
+                            else walk[((parity ^ 1) * G::CW + w) * 64] = r;
                         }
                         parity ^= 1;
                         --dd;
                     }
                     if (dd == 0) root_par = parity;
-                    else brow = set_range(brow, own, dd, dd + 1);
-                    ws_sync();
+                    else brow = set_field(brow, dd, slot);
                 }
             }
             lds_sync();
-            STAMP(3);
+            STAMP(5);
         }
 
         // ================================================ best path, output
         int best = 0;
         if constexpr (!SC) {
-            double2* metv = reinterpret_cast<double2*>(smem + G::L_MET);
-            metv[lane] = make_double2(pm, 0.0);
+            met[slot] = make_double2(pm, 0.0);
             lds_sync();
-            double bm = metv[base].x;
+            double bm = met[0].x;
             for (int q = 1; q < nact; ++q) {
-                const double v = metv[base + q].x;
+                const double v = met[q].x;
                 if (v > bm) { bm = v; best = q; }
             }
             lds_sync();
         }
+        ws_sync();  // the root partial sum was written to the walk buffer
         uint32_t* X = reinterpret_cast<uint32_t*>(smem + G::L_FINAL) + fw * G::CW;
-        const uint32_t* walk = reinterpret_cast<const uint32_t*>(ws + G::W_WALK) + lane;
         if (slot == best)
             for (int w = 0; w < G::CW; ++w) X[w] = polar_word_transform(walk[(root_par * G::CW + w) * 64]);
         lds_sync();
@@ -425,11 +448,12 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
             }
         }
         lds_sync();
-        STAMP(4);
+        ws_sync();  // staging of the next frames overwrites workspace read above
+        STAMP(6);
     }
     if constexpr (STAMPS) {
         if (lane == 0)
-            for (int k = 0; k < 5; ++k) atomicAdd(stamps + k, acc[k]);
+            for (int k = 0; k < 8; ++k) atomicAdd(stamps + k, acc[k]);
     }
 #undef STAMP
 }

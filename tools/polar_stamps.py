@@ -22,12 +22,12 @@ msg = torch.empty((a.batch, K), dtype=torch.uint8, device="cuda"); _native.rando
 cw = torch.empty((a.batch, N), dtype=torch.uint8, device="cuda"); _native.polar_encode(plan, msg, cw)
 llr = AWGNChannel(a.snr).llr_batch_device(cw, N, a.batch, seed=42)
 out = torch.empty((a.batch, K), dtype=torch.uint8, device="cuda")
-st = torch.zeros(5, dtype=torch.int64, device="cuda")
+st = torch.zeros(8, dtype=torch.int64, device="cuda")
 plan.decode_stamped(llr, out, st); torch.cuda.synchronize(); st.zero_()
 t = time.perf_counter(); plan.decode_stamped(llr, out, st); torch.cuda.synchronize(); dt = time.perf_counter() - t
 s = st.cpu().numpy().astype(float)
 ok = bool(torch.equal(out, msg)) if a.snr > 20 else None
-names = ["llr_update", "metrics", "prune_clone", "beta_walk", "final"]
+names = ["fused_top", "ws_chains", "lds_chain", "metrics", "prune_clone", "beta_walk", "final", "ws_sync"] if plan.info.reserved == 4 else ["llr_update", "metrics", "prune_clone", "beta_walk", "final"]
 print(json.dumps({"N": N, "L": a.list_size, "fused": plan.info.fused_top, "lds": plan.info.lds_bytes,
                   "stamped_ms": dt * 1e3, "cycles_per_frame": s.sum() / a.batch,
-                  "share": {k: v / s.sum() for k, v in zip(names, s)}}))
+                  "share": {k: round(v / s.sum(), 4) for k, v in zip(names, s)}}))

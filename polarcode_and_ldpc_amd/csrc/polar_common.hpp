@@ -8,14 +8,20 @@
 
 namespace pl {
 
-// min-sum f with the reference's value semantics: sign(a)*sign(b)*min(|a|,|b|);
-// zeros give a zero, NaN in either input gives NaN.  Exact (no rounding).
+// min-sum f with the reference's value semantics: sign(a)*sign(b)*min(|a|,|b|)
+// (Python min keeps |a| unless |b| < |a|); NaN in either input gives NaN.  The
+// sign of a zero result may differ from NumPy's, which never changes a value or
+// decision downstream (x + -0 = x + 0 for x != 0, and -0 >= 0).  Exact.
+// 7 VALU: cmp, 2 selects, xor + bfi for the sign, unordered cmp + select.
 PL_DEV double f_ms(double a, double b) {
-    const double x = fabs(a), y = fabs(b);
-    const double mn = (y < x) ? y : x;
-    const uint64_t sb = ((uint64_t)__double_as_longlong(a) ^ (uint64_t)__double_as_longlong(b)) & 0x8000000000000000ull;
-    const double r = __longlong_as_double((long long)((uint64_t)__double_as_longlong(mn) | sb));
-    return __builtin_isunordered(a, b) ? __builtin_nan("") : r;
+    const bool lt = fabs(b) < fabs(a);
+    const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
+    const uint32_t lo = lt ? (uint32_t)ub : (uint32_t)ua;
+    const uint32_t hs = lt ? (uint32_t)(ub >> 32) : (uint32_t)(ua >> 32);
+    const uint32_t sg = (uint32_t)(ua >> 32) ^ (uint32_t)(ub >> 32);
+    uint32_t hi = (hs & 0x7FFFFFFFu) | (sg & 0x80000000u);
+    hi = __builtin_isunordered(a, b) ? 0x7FF80000u : hi;
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 // g: btm + top if bit == 0 else btm - top (one rounding, as the reference)
 PL_DEV double g_op(double top, double btm, uint32_t bit) {
@@ -35,6 +41,26 @@ PL_DEV void path_metrics(double pm, double lam, double& m0, double& m1) {
     e = e < ex ? e : ex;
     e = e < -1100 ? -1100 : (e > 1100 ? 1100 : e);  // ilogb(0) = INT_MIN: keep 56 - e finite
     const bool skip = (pm != 0.0) && (x > (double)(56 - e) * 0.6931471805599453);
+    double t = 0.0;
+    if (!skip) t = log1p(exp(-x));
+    m0 = pm + ((lam >= 0.0) ? -t : lam - t);
+    if (WANT1) m1 = pm + ((lam >= 0.0) ? -lam - t : -t);
+}
+
+// Same increments for the tree kernel, with a cheaper skip test (hardware
+// frexp exponents: frexp_exp = ilogb + 1 for finite nonzero values, so the
+// threshold is identical) and two more skips that cannot change a result:
+// inactive list slots (their metrics are never read) and pm = +-inf with a
+// non-NaN LLR (t is finite, so pm + anything finite = pm as in the reference).
+template <bool WANT1>
+PL_DEV void path_metrics_fast(double pm, double lam, bool active, double& m0, double& m1) {
+    const double x = fabs(lam);
+    const int ep = __builtin_amdgcn_frexp_exp(pm);
+    const int ex = __builtin_amdgcn_frexp_exp(x);
+    const int e = ep < ex ? ep : ex;
+    const bool finite_pm = __builtin_isfinite(pm);
+    const bool skip = !active || (!finite_pm && !__builtin_isnan(x)) ||
+                      (finite_pm && pm != 0.0 && x > (double)(57 - e) * 0.6931471805599453);
     double t = 0.0;
     if (!skip) t = log1p(exp(-x));
     m0 = pm + ((lam >= 0.0) ? -t : lam - t);

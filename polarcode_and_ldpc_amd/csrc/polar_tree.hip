@@ -35,6 +35,8 @@
 #include "internal.hpp"
 #include "polar_common.hpp"
 
+#include <cstdlib>
+
 namespace pl {
 
 namespace {
@@ -235,8 +237,8 @@ PL_DEV double descend_from(int p, unsigned char* smem, unsigned char* ws, int la
 
 }  // namespace
 
-template <int NL, int LCAP, bool SC, int F, int DL, bool STAMPS>
-__global__ void __launch_bounds__(64)
+template <int NL, int LCAP, bool SC, int F, int DL, bool STAMPS, int WPE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restrict__ out,
                   const uint32_t* __restrict__ frozen_dec, const int32_t* __restrict__ info_pos, int64_t batch,
                   int K, int Lsz, unsigned char* __restrict__ workspace, unsigned long long* __restrict__ stamps) {
@@ -315,13 +317,13 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 STAMP(3);
             } else if (frozen) {
                 double m0, m1;
-                path_metrics<false>(pm, lam, m0, m1);
+                path_metrics_fast<false>(pm, lam, slot < nact, m0, m1);
                 if (slot < nact) pm = m0;
                 bit = 0;
                 STAMP(3);
             } else {
                 double m0, m1;
-                path_metrics<true>(pm, lam, m0, m1);
+                path_metrics_fast<true>(pm, lam, slot < nact, m0, m1);
                 STAMP(3);
                 met[slot] = make_double2(m0, m1);
                 rowx[2 * slot] = lrow;
@@ -467,6 +469,7 @@ struct TreeEntry {
     int F, DL;
     void* fn;
     void* fn_stamps;
+    void* fn_occ4;  // same kernel compiled for 4 waves/SIMD (128 VGPRs), PL_TREE_WPE=4
     int lds;
     int64_t ws;
 };
@@ -474,13 +477,16 @@ struct TreeEntry {
 template <int NL, int LCAP, bool SC, int F, int DL>
 TreeEntry make_entry() {
     using G = TG<NL, LCAP, F, DL>;
-    return TreeEntry{NL, LCAP, SC, F, DL, (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false>,
-                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, true>, G::LDS, G::WS};
+    return TreeEntry{NL, LCAP, SC, F, DL, (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 1>,
+                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, true, 3>,
+                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 4>, G::LDS, G::WS};
 }
 
 const TreeEntry* tree_table(int* count) {
     static const TreeEntry tab[] = {
         make_entry<10, 8, false, 3, 7>(),
+        make_entry<10, 8, false, 2, 7>(),
+        make_entry<10, 8, false, 4, 7>(),
     };
     *count = (int)(sizeof(tab) / sizeof(tab[0]));
     return tab;
@@ -491,9 +497,12 @@ const TreeEntry* tree_table(int* count) {
 bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info) {
     int cnt = 0;
     const TreeEntry* t = tree_table(&cnt);
+    const char* fe = std::getenv("PL_TREE_F");  // diagnostic: pick the fused-top depth
+    const int want_f = fe ? std::atoi(fe) : 0;
     for (int k = 0; k < cnt; ++k)
-        if (t[k].n == n && t[k].lcap == lcap && t[k].sc == sc) {
-            info->fn = t[k].fn;
+        if (t[k].n == n && t[k].lcap == lcap && t[k].sc == sc && (!want_f || t[k].F == want_f)) {
+            const char* w = std::getenv("PL_TREE_WPE");
+            info->fn = (w && std::atoi(w) == 4) ? t[k].fn_occ4 : t[k].fn;
             info->fn_stamps = t[k].fn_stamps;
             info->lds_bytes = t[k].lds;
             info->ws_bytes = t[k].ws;

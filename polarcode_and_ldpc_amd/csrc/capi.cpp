@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -229,11 +230,33 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     int maxdv = 0;
     for (int v = 0; v < n; ++v) maxdv = std::max(maxdv, var_ptr[v + 1] - var_ptr[v]);
     if (maxdv > 128) return fail(PL_EUNSUPPORTED, "variable degree > 128");
+    // Device edge order: checks sorted by degree (stable), so the lanes of a
+    // wavefront run check loops of equal length; columns stay ascending within a
+    // check (the reference's product order).  No result depends on the check
+    // order: var_edge lists each variable's edges by ascending ORIGINAL check
+    // index, the order of the reference's np.sum over them (decoder.py:110-116).
+    std::vector<int32_t> order(m);
+    for (int c = 0; c < m; ++c) order[c] = c;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        return (row_ptr[a + 1] - row_ptr[a]) < (row_ptr[b + 1] - row_ptr[b]);
+    });
+    std::vector<int32_t> prow(m + 1, 0), pcol(E), new_edge(E);  // new_edge[original edge]
+    for (int k = 0; k < m; ++k) {
+        const int c = order[k];
+        prow[k + 1] = prow[k] + (row_ptr[c + 1] - row_ptr[c]);
+        for (int e = row_ptr[c], j = prow[k]; e < row_ptr[c + 1]; ++e, ++j) {
+            pcol[j] = col_idx[e];
+            new_edge[e] = j;
+            edge_chk[j] = k;
+        }
+    }
     {
         std::vector<int32_t> fill(var_ptr.begin(), var_ptr.end() - 1);
-        for (int c = 0; c < m; ++c)
-            for (int e = row_ptr[c]; e < row_ptr[c + 1]; ++e) var_edge[fill[col_idx[e]]++] = e;
+        for (int c = 0; c < m; ++c)  // original check order
+            for (int e = row_ptr[c]; e < row_ptr[c + 1]; ++e) var_edge[fill[col_idx[e]]++] = new_edge[e];
     }
+    row_ptr = prow.data();
+    col_idx = pcol.data();
     pl_plan* p = new pl_plan();
     p->kind = 1;
     hipGetDevice(&p->device);
@@ -244,6 +267,13 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     const size_t lds_all = (size_t)(2 * (size_t)E + n) * 8 + n;
     g.use_global = lds_all > 64 * 1024 ? 1 : 0;
     g.lds_bytes = (int)(((g.use_global ? (size_t)n : lds_all) + 15) & ~(size_t)15);
+    // check-per-thread kernel (ldpc.hip ldpc_check_kernel): diagnostic, PL_LDPC_KERNEL=check
+    const char* lk = std::getenv("PL_LDPC_KERNEL");
+    g.check_kernel = !g.use_global && lk && std::string(lk) == "check" ? 1 : 0;
+    if (g.check_kernel) {
+        g.threads = 256;
+        g.lds_bytes = (int)(((size_t)(2 * (size_t)E + n) * 8 + 15) & ~(size_t)15);
+    }
     std::vector<int32_t> all;
     all.insert(all.end(), row_ptr, row_ptr + m + 1);
     all.insert(all.end(), col_idx, col_idx + E);

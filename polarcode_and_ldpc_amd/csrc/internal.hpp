@@ -77,6 +77,7 @@ struct LdpcGeom {
     int threads;       // threads per workgroup (one frame per workgroup)
     int lds_bytes;     // 0 => messages live in the global workspace
     int use_global;
+    int check_kernel;  // 1: ldpc_check_kernel (thread per check, state in LDS)
 };
 struct LdpcDev {
     const int32_t* row_ptr;   // [m+1]

@@ -21,11 +21,89 @@
 #include "common.hpp"
 #include "internal.hpp"
 
+#include <cstdlib>
+#include <string>
+
 namespace pl {
 
 PL_DEV double clip999(double x) {
     const double c = 0.999999;
     return x < -c ? -c : (x > c ? c : x);
+}
+
+
+// ---- lean fp64 transcendentals for the BP check update ---------------------
+// The reference evaluates np.tanh / np.arctanh (NumPy's SIMD kernels); ocml's
+// versions cost ~160 VALU each (double-double internals) and made this kernel
+// VALU-bound.  These are <= ~2 ulp (NumPy's own differ from libm by 1-2 ulp in
+// ~20 % of inputs), and decisions are checked bit-exact against the
+// reference fixtures (tests/test_gpu_ldpc.py).  PL_LDPC_MATH=ocml restores ocml.
+//
+// log1p for x >= 0: the classic reduction 1+x = 2^k (1+f), sqrt(2)/2 <= 1+f <
+// sqrt(2), with the rounding of 1+x carried as a correction c, and log(1+f) =
+// 2s + s R(s^2), s = f/(2+f), R the published minimax fit (Lg1..Lg7, the
+// coefficients of the Sun fdlibm log kernel).
+// x / y to <= 1 ulp: hardware reciprocal, two Newton steps, one residual step
+// (8 VALU against 13 for the IEEE-exact sequence); y finite, nonzero, normal.
+PL_DEV double div_fast(double x, double y) {
+    double r = __builtin_amdgcn_rcp(y);
+    double e = fma(-y, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-y, r, 1.0);
+    r = fma(r, e, r);
+    const double q = x * r;
+    return fma(fma(-y, q, x), r, q);
+}
+PL_DEV double lg_R(double z) {
+    const double w = z * z;
+    const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
+    const double t2 = z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01),
+                                     2.857142874366239149e-01), 6.666666666666735130e-01);
+    return t2 + t1;
+}
+PL_DEV double log1p_pos(double x) {
+    constexpr double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+    double f, c = 0.0;
+    int k = 0;
+    if (x < 0.41421356237309503) {
+        f = x;
+    } else {
+        const double u = 1.0 + x;
+        k = __builtin_amdgcn_frexp_exp(u) - 1;  // u = 2^k * m, m in [1, 2)
+        c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0);
+        c *= __builtin_amdgcn_rcp(u);  // rounding correction, a few bits suffice
+        double m = __builtin_amdgcn_ldexp(u, -k);
+        if (m >= 1.4142135623730951) { m *= 0.5; k += 1; }
+        f = m - 1.0;
+    }
+    const double hfsq = 0.5 * f * f;
+    const double s = div_fast(f, 2.0 + f);
+    const double R = lg_R(s * s);
+    if (k == 0) return f - (hfsq - s * (hfsq + R));
+    const double dk = (double)k;
+    return dk * LN2_HI - ((hfsq - (s * (hfsq + R) + (dk * LN2_LO + c))) - f);
+}
+// 2*atanh(p), |p| <= 0.999999 (after the reference's clip), NaN -> NaN:
+// 2 atanh(a) = log1p(2a + 2a*a/(1-a)) (a < 0.5) or log1p(2a/(1-a)).
+PL_DEV double two_atanh(double p) {
+    const double a = fabs(p);
+    const double q = div_fast(a, 1.0 - a);  // 1 - a >= 1e-6
+    const double t = a + a;
+    const double w = (a < 0.5) ? t + t * q : q + q;  // one log1p for the whole wave
+    const double r = log1p_pos(w);
+    return __builtin_isnan(p) ? p : __builtin_copysign(r, p);
+}
+// clip(tanh(x/2), +-0.999999): tanh(|x|/2) = -em/(2+em), em = expm1(-|x|); for
+// |x| > 30 tanh is above the clip bound.
+PL_DEV double tanh_half_clip(double x) {
+    const double ax = fabs(x);
+    double t = 0.999999;
+    if (ax <= 30.0) {
+        const double em = expm1(-ax);
+        t = div_fast(-em, 2.0 + em);
+        t = t > 0.999999 ? 0.999999 : t;
+    }
+    return __builtin_isnan(x) ? x : __builtin_copysign(t, x);
 }
 
 // numpy add.reduce (pairwise_sum) over msgs gathered through var_edge.
@@ -48,7 +126,7 @@ PL_DEV double np_sum_gather(const double* C, const int32_t* __restrict__ ve, int
     return res;
 }
 
-template <int ALGO, bool GLOBAL>
+template <int ALGO, bool GLOBAL, bool OCML>
 __global__ void __launch_bounds__(1024)
 ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
                    uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch,
@@ -74,7 +152,7 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
         // check inputs v2c = total - c2v
         for (int e = tid; e < E; e += nt) {
             const double x = tot[dv.col_idx[e]] - C[e];
-            T[e] = (ALGO == 0) ? clip999(tanh(x / 2.0)) : x;
+            T[e] = (ALGO == 0) ? (OCML ? clip999(tanh(x / 2.0)) : tanh_half_clip(x)) : x;
         }
         __syncthreads();
         // leave-one-out check outputs
@@ -87,7 +165,7 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
                 for (int k = 0; k < d; ++k)
                     if (k != i) p *= T[e0 + k];
                 p = clip999(p);
-                o = 2.0 * atanh(p);
+                o = OCML ? 2.0 * atanh(p) : two_atanh(p);
                 if (isnan(o)) o = 0.0;
                 else if (isinf(o)) o = o > 0.0 ? 20.0 : -20.0;
             } else {
@@ -133,23 +211,123 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
     if (iters && tid == 0) iters[frame] = done;
 }
 
+
+// Thread-per-check kernel: one workgroup (256 threads) per frame, all state in
+// LDS: C[E] (check-to-variable), T[E] (check inputs), tot[n].  Checks are
+// degree-sorted by the host so a wavefront's check loops have equal length.
+// Per iteration:
+//   check pass (thread = check): x_k = tot[v_k] - C[e_k] (v2c as the reference
+//     forms it), T = clip(tanh(x/2)) (BP) or x (MS); leave-one-out outputs with
+//     the running prefix product shared: p_i = (t_0...t_{i-1}) * t_{i+1} * ...,
+//     the same left-to-right order as np.prod over the masked messages; the
+//     syndrome of the decisions of tot (the previous iteration's) rides along;
+//   vote (__syncthreads_or): all checks satisfied -> stop (iterations = it);
+//   variable pass (thread = variable): tot = llr + np.sum(C over its checks).
+// Two barriers per iteration (the reference's check / variable / decision /
+// syndrome sequence, decoder.py:148-198, with the syndrome of iteration it
+// evaluated at the start of iteration it+1 -- same stop point, same bits).
+template <int ALGO>
+__global__ void __launch_bounds__(256)
+ldpc_check_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
+                  uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int E = g.E, n = g.n, m = g.m;
+    double* C = reinterpret_cast<double*>(smem);
+    double* T = C + E;
+    double* tot = T + E;
+    const int32_t* __restrict__ rp = dv.row_ptr;
+    const int32_t* __restrict__ ci = dv.col_idx;
+    for (int64_t frame = blockIdx.x; frame < batch; frame += gridDim.x) {
+        const double* __restrict__ ch = llr + frame * ld;
+        for (int e = tid; e < E; e += nt) C[e] = 0.0;
+        for (int v = tid; v < n; v += nt) tot[v] = ch[v];  // decoder.py:144-146 (v2c = llr)
+        __syncthreads();
+        int done = g.max_iter;
+        for (int it = 0; it < g.max_iter; ++it) {
+            int syn = 0;
+            for (int c = tid; c < m; c += nt) {
+                const int e0 = rp[c], d = rp[c + 1] - e0;
+                int s = 0;
+                for (int k = 0; k < d; ++k) {
+                    const double tv = tot[ci[e0 + k]];
+                    s ^= (tv <= 0.0) ? 1 : 0;
+                    const double x = tv - C[e0 + k];
+                    T[e0 + k] = (ALGO == 0) ? tanh_half_clip(x) : x;
+                }
+                syn |= s;
+                if (ALGO == 0) {
+                    double P = 1.0;  // t_0 * ... * t_{i-1}, sequential
+                    for (int i = 0; i < d; ++i) {
+                        double p = P;
+                        for (int k = i + 1; k < d; ++k) p *= T[e0 + k];
+                        p = clip999(p);
+                        double o = two_atanh(p);
+                        if (isnan(o)) o = 0.0;
+                        else if (isinf(o)) o = o > 0.0 ? 20.0 : -20.0;
+                        C[e0 + i] = o;
+                        P *= T[e0 + i];
+                    }
+                } else {
+                    for (int i = 0; i < d; ++i) {
+                        double sp = 1.0, mn = 0.0;
+                        bool first = true;
+                        for (int k = 0; k < d; ++k) {
+                            if (k == i) continue;
+                            const double x = T[e0 + k];
+                            sp *= np_sign(x);
+                            const double ax = fabs(x);
+                            if (first) { mn = ax; first = false; }
+                            else if (isnan(ax) || isnan(mn)) mn = __builtin_nan("");
+                            else if (ax < mn) mn = ax;
+                        }
+                        C[e0 + i] = sp * mn * g.norm;
+                    }
+                }
+            }
+            if (g.early_stop && it > 0) {
+                if (!__syncthreads_or(syn)) { done = it; break; }
+            } else {
+                __syncthreads();
+            }
+            for (int v = tid; v < n; v += nt) {
+                const int a0 = dv.var_ptr[v], d = dv.var_ptr[v + 1] - a0;
+                tot[v] = ch[v] + np_sum_gather(C, dv.var_edge + a0, d);
+            }
+            __syncthreads();
+        }
+        uint8_t* o = bits + frame * (int64_t)n;
+        for (int v = tid; v < n; v += nt) o[v] = tot[v] <= 0.0 ? 1 : 0;
+        if (iters && tid == 0) iters[frame] = done;
+        __syncthreads();
+    }
+}
+
 size_t ldpc_work_bytes_per_frame(const LdpcGeom& g) {
     return g.use_global ? (size_t)(2 * (size_t)g.E + g.n) * sizeof(double) : 0;
 }
 
 template <int ALGO>
 static void* pick(bool global) {
-    return global ? (void*)ldpc_decode_kernel<ALGO, true> : (void*)ldpc_decode_kernel<ALGO, false>;
+    const char* m = std::getenv("PL_LDPC_MATH");
+    if (ALGO == 0 && m && std::string(m) == "ocml")
+        return global ? (void*)ldpc_decode_kernel<ALGO, true, true> : (void*)ldpc_decode_kernel<ALGO, false, true>;
+    return global ? (void*)ldpc_decode_kernel<ALGO, true, false> : (void*)ldpc_decode_kernel<ALGO, false, false>;
+}
+
+static void* pick_kernel(const LdpcGeom& g) {
+    if (g.check_kernel) return g.algo == 0 ? (void*)ldpc_check_kernel<0> : (void*)ldpc_check_kernel<1>;
+    return g.algo == 0 ? pick<0>(g.use_global) : pick<1>(g.use_global);
 }
 
 hipError_t ldpc_prepare(const LdpcGeom& g) {
-    void* k = g.algo == 0 ? pick<0>(g.use_global) : pick<1>(g.use_global);
+    void* k = pick_kernel(g);
     return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds_bytes);
 }
 
 hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, int64_t ld,
                        uint8_t* bits, int32_t* iters, int64_t batch, double* work, hipStream_t s) {
-    void* k = g.algo == 0 ? pick<0>(g.use_global) : pick<1>(g.use_global);
+    void* k = pick_kernel(g);
     LdpcGeom gg = g;
     LdpcDev dd = d;
     void* args[] = {&gg, &dd, (void*)&llr, (void*)&ld, (void*)&bits, (void*)&iters, (void*)&batch,

@@ -1,6 +1,7 @@
-# usage: bash tools/gpu_pmc2.sh <tag>   SQ/TA/TD/TCP counter passes over the polar bench (one launch + 3 timed)
+# usage: bash tools/gpu_pmc2.sh <tag> [script args...]   SQ/TA/TD/TCP counter passes (default: polar bench)
 set -o pipefail
-TAG=${1:-pmc}
+TAG=${1:-pmc}; shift
+if [ $# -gt 0 ]; then CMD=("$@"); else CMD=(bench.py --skip-cpu --skip-ldpc --steps 1 --warmup 0); fi
 R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/pmc2_$TAG"; mkdir -p "$OUT"
 export TMPDIR=/tmp; cd /tmp
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
@@ -11,5 +12,5 @@ i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
   timeout -k 10 -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$OUT/p$i" -o run -- \
-      python3 "$R/bench.py" --skip-cpu --skip-ldpc --steps 1 --warmup 0 > "$OUT/p$i.out" 2> "$OUT/p$i.err" || echo "pass $i failed $?" >> "$OUT/fail.txt"
+      python3 "$R/${CMD[0]}" "${CMD[@]:1}" > "$OUT/p$i.out" 2> "$OUT/p$i.err" || echo "pass $i failed $?" >> "$OUT/fail.txt"
 done

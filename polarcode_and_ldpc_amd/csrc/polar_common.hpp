@@ -5,6 +5,7 @@
 //   metric increments src/polar/decoder.py:374-406 (SCLDecoder._log_likelihood)
 #pragma once
 #include "common.hpp"
+#include "fp64_math.hpp"
 
 namespace pl {
 
@@ -62,7 +63,7 @@ PL_DEV void path_metrics_fast(double pm, double lam, bool active, double& m0, do
     const bool skip = !active || (!finite_pm && !__builtin_isnan(x)) ||
                       (finite_pm && pm != 0.0 && x > (double)(57 - e) * 0.6931471805599453);
     double t = 0.0;
-    if (!skip) t = log1p(exp(-x));
+    if (!skip) t = log1p_pos(exp(-x));  // lean log1p (fp64_math.hpp), exp(-x) in [0, 1]
     m0 = pm + ((lam >= 0.0) ? -t : lam - t);
     if (WANT1) m1 = pm + ((lam >= 0.0) ? -lam - t : -t);
 }

@@ -110,3 +110,21 @@ def test_full_batch_bp_device(gpu):
     want_b, want_i = O.ldpc_decode(rp, ci, 504, llr[idx].cpu().numpy(), max_iter=20, threads=8)
     assert np.array_equal(bits[idx].cpu().numpy().astype(np.int64), want_b)
     assert np.array_equal(its[idx].cpu().numpy(), want_i)
+
+
+def test_bp_lean_math_stress_vs_oracle(gpu, oracle):
+    """The BP kernel's own fp64 tanh/atanh (ldpc.hip) against the oracle's libm on
+    1024 frames around the waterfall (-1..2.5 dB), where messages hover near
+    decision boundaries longest: every decision and iteration count equal."""
+    L = _L()
+    H = L.mackay_construction(504, 252, 3, 6, 42)
+    rp, ci = L.dense_to_csr(H)
+    rng = np.random.RandomState(2024)
+    B = 1024
+    snr = rng.uniform(-1.0, 2.5, size=(B, 1))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+    llr = 2.0 * (1.0 + sigma * rng.randn(B, 504)) / sigma ** 2
+    want_b, want_i = oracle.ldpc_decode(rp, ci, 504, llr, algo="bp", max_iter=20, early_stop=True, threads=16)
+    got_b, got_i = L.BPDecoder(H, 20, True).decode_batch(llr, return_iterations=True)
+    assert np.array_equal(got_b, want_b)
+    assert np.array_equal(got_i, want_i)

@@ -64,7 +64,14 @@ struct TG {
     static constexpr int L_END1 = L_FINAL + FPW * CW * 4;
     static constexpr int LDS = (((L_END0 > L_END1) ? L_END0 : L_END1) + 15) & ~15;
     // ---- workspace (bytes per wave)
-    static constexpr int64_t W_CH_BYTES = STAGE ? (int64_t)N * FPW * 8 : 0;  // [N/2][FPW] f64 pairs
+    // staged channel depth 0 and its path-independent f-only depths 1..NS
+    // (the left-most nodes): depth d as [S_d/2][FPW] f64 pairs at st_off(d)
+    static constexpr int NS = STAGE ? (F - 1 < 2 ? F - 1 : 2) : 0;
+    static constexpr int64_t W_CH_BYTES =
+        STAGE ? (int64_t)FPW * 8 * (N + (NS >= 1 ? N / 2 : 0) + (NS >= 2 ? N / 4 : 0)) : 0;
+    static constexpr int64_t st_off(int d) {
+        return (int64_t)FPW * 8 * ((d >= 1 ? N : 0) + (d >= 2 ? N / 2 : 0));
+    }
     static constexpr int64_t W_LLR = W_CH_BYTES;                               // pools F..DL-1
     static constexpr int64_t W_LLR_BYTES = 1024LL * ((1LL << (n - F)) - (1LL << (n - DL)));
     static constexpr int64_t W_BL = W_LLR + W_LLR_BYTES;  // beta depths 1..NB: [W_d][64] u32
@@ -173,40 +180,33 @@ PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int lane, int ps
     return st.lam;
 }
 
-// Fused top: depth-F elements from 2^F channel values each (level d is g where
-// the depth-d ancestor of leaf i is a right child), then the f-chain to the leaf.
-template <class G>
-PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, int fw, int i, const double* ch,
-                            uint64_t brow, int base, uint32_t bb, uint32_t bw5) {
-    constexpr int n = G::n, F = G::F, SF = 1 << (n - F);
+// Fused top from staged depth D0 (0 = channel; 1, 2 = the path-independent
+// left-most f-only nodes, valid when the ancestors at depths 1..D0 are left
+// children): depth-F elements from 2^(F-D0) values each (level d is g where the
+// depth-d ancestor of leaf i is a right child), then the f-chain to the leaf.
+template <class G, int D0>
+PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int fw, const double* ch,
+                         const bool* right, const uint32_t* const* bsrc, uint32_t* bw) {
+    constexpr int n = G::n, F = G::F, SF = 1 << (n - F), W = 1 << (F - D0);
     Fold<G> st;
     st.lam = 0.0;
-    bool right[F + 1];
-    const uint32_t* bsrc[F + 1];
-    uint32_t bw[F + 1];
-#pragma unroll
-    for (int d = 1; d <= F; ++d) {
-        right[d] = (i >> (n - d)) & 1;
-        bsrc[d] = reinterpret_cast<const uint32_t*>(ws + G::bl_off(d <= G::NB ? d : 1)) + base + field(brow, d);
-        bw[d] = (d > G::NB) ? beta_get<n>(d, bb, bw5) : 0u;
-    }
-    const double2* chs = reinterpret_cast<const double2*>(ws) + fw;  // staged [N/2][FPW]
+    const double2* src = reinterpret_cast<const double2*>(ws + G::st_off(D0)) + fw;
 #pragma unroll 2
     for (int t = 0; t < SF; ++t) {
-        double v[1 << F];
+        double v[W];
         if constexpr (G::STAGE) {
 #pragma unroll
-            for (int k = 0; k < (1 << (F - 1)); ++k) {
-                const double2 pr = chs[((t << (F - 1)) + k) * G::FPW];
+            for (int k = 0; k < W / 2; ++k) {
+                const double2 pr = src[((t * (W / 2)) + k) * G::FPW];
                 v[2 * k] = pr.x;
                 v[2 * k + 1] = pr.y;
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < (1 << F); ++k) v[k] = ch[(t << F) + k];
+            for (int k = 0; k < W; ++k) v[k] = ch[t * W + k];
         }
 #pragma unroll
-        for (int d = 1; d <= F; ++d) {
+        for (int d = D0 + 1; d <= F; ++d) {
             const int e0 = t << (F - d);  // depth-d element index of v[0]
             const int m = 1 << (F - d);
             if (right[d]) {
@@ -222,6 +222,28 @@ PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, in
         fold<G, F>(st, v[0], t, smem, ws, lane);
     }
     return st.lam;
+}
+
+template <class G>
+PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, int fw, int i, const double* ch,
+                            uint64_t brow, int base, uint32_t bb, uint32_t bw5) {
+    constexpr int n = G::n, F = G::F;
+    bool right[F + 1];
+    const uint32_t* bsrc[F + 1];
+    uint32_t bw[F + 1];
+#pragma unroll
+    for (int d = 1; d <= F; ++d) {
+        right[d] = (i >> (n - d)) & 1;
+        bsrc[d] = reinterpret_cast<const uint32_t*>(ws + G::bl_off(d <= G::NB ? d : 1)) + base + field(brow, d);
+        bw[d] = (d > G::NB) ? beta_get<n>(d, bb, bw5) : 0u;
+    }
+    if constexpr (G::NS >= 2) {
+        if (!right[1] && !right[2]) return fused_loop<G, 2>(smem, ws, lane, fw, ch, right, bsrc, bw);
+    }
+    if constexpr (G::NS >= 1) {
+        if (!right[1]) return fused_loop<G, 1>(smem, ws, lane, fw, ch, right, bsrc, bw);
+    }
+    return fused_loop<G, 0>(smem, ws, lane, fw, ch, right, bsrc, bw);
 }
 
 template <class G, int P>
@@ -271,16 +293,32 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         const bool live = frame < batch;
         const double* __restrict__ ch = llr + (live ? frame : batch - 1) * ld;
         if constexpr (G::STAGE) {
-            // channel rows of this wave's frames -> [N/2][FPW] pairs (lane: frame l%FPW)
+            // channel rows of this wave's frames -> [N/2][FPW] pairs, plus the
+            // path-independent left-most nodes f(ch) and f(f(ch)) (depths 1, 2).
+            // Lane: frame l % FPW, 8 consecutive channel values per step.
             const int sf = lane % FPW;
             const int64_t fr = f0 + sf < batch ? f0 + sf : batch - 1;
             const double* row = llr + fr * ld;
-            double2* dst = reinterpret_cast<double2*>(ws);
-            constexpr int PPI = 64 / FPW;  // pairs per frame per instruction
-#pragma unroll 4
-            for (int pb = 0; pb < N / 2; pb += PPI) {
-                const int pr = pb + lane / FPW;
-                dst[pr * FPW + sf] = make_double2(row[2 * pr], row[2 * pr + 1]);
+            double2* d0 = reinterpret_cast<double2*>(ws + G::st_off(0)) + sf;
+            double2* d1 = reinterpret_cast<double2*>(ws + G::st_off(1)) + sf;
+            double2* d2 = reinterpret_cast<double2*>(ws + G::st_off(2)) + sf;
+            constexpr int CPI = 64 / FPW;  // 8-value chunks per frame per step
+#pragma unroll 2
+            for (int cb = 0; cb < N / 8; cb += CPI) {
+                const int cc = cb + lane / FPW;
+                double v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = row[8 * cc + k];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) d0[(4 * cc + k) * FPW] = make_double2(v[2 * k], v[2 * k + 1]);
+                if constexpr (G::NS >= 1) {
+                    double u[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) u[k] = f_ms(v[2 * k], v[2 * k + 1]);
+                    d1[(2 * cc) * FPW] = make_double2(u[0], u[1]);
+                    d1[(2 * cc + 1) * FPW] = make_double2(u[2], u[3]);
+                    if constexpr (G::NS >= 2) d2[cc * FPW] = make_double2(f_ms(u[0], u[1]), f_ms(u[2], u[3]));
+                }
             }
         }
         uint64_t lrow = own, brow = own;
@@ -467,9 +505,10 @@ struct TreeEntry {
     int n, lcap;
     bool sc;
     int F, DL;
-    void* fn;
+    void* fn;         // compiled for 4 waves/SIMD (<= 128 VGPRs; measured fastest)
     void* fn_stamps;
-    void* fn_occ4;  // same kernel compiled for 4 waves/SIMD (128 VGPRs), PL_TREE_WPE=4
+    void* fn_wpe1;    // compiler's own register budget (3 waves/SIMD), PL_TREE_WPE=1
+    void* fn_wpe5;    // 5 waves/SIMD (<= 96 VGPRs), PL_TREE_WPE=5
     int lds;
     int64_t ws;
 };
@@ -477,9 +516,10 @@ struct TreeEntry {
 template <int NL, int LCAP, bool SC, int F, int DL>
 TreeEntry make_entry() {
     using G = TG<NL, LCAP, F, DL>;
-    return TreeEntry{NL, LCAP, SC, F, DL, (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 1>,
-                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, true, 3>,
-                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 4>, G::LDS, G::WS};
+    return TreeEntry{NL, LCAP, SC, F, DL, (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 4>,
+                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, true, 4>,
+                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 1>,
+                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 5>, G::LDS, G::WS};
 }
 
 const TreeEntry* tree_table(int* count) {
@@ -502,7 +542,8 @@ bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info) {
     for (int k = 0; k < cnt; ++k)
         if (t[k].n == n && t[k].lcap == lcap && t[k].sc == sc && (!want_f || t[k].F == want_f)) {
             const char* w = std::getenv("PL_TREE_WPE");
-            info->fn = (w && std::atoi(w) == 4) ? t[k].fn_occ4 : t[k].fn;
+            const int wpe = w ? std::atoi(w) : 4;
+            info->fn = wpe == 1 ? t[k].fn_wpe1 : (wpe == 5 ? t[k].fn_wpe5 : t[k].fn);
             info->fn_stamps = t[k].fn_stamps;
             info->lds_bytes = t[k].lds;
             info->ws_bytes = t[k].ws;

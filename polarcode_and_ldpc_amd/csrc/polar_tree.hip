@@ -508,25 +508,33 @@ struct TreeEntry {
     void* fn;         // compiled for 4 waves/SIMD (<= 128 VGPRs; measured fastest)
     void* fn_stamps;
     void* fn_wpe1;    // compiler's own register budget (3 waves/SIMD), PL_TREE_WPE=1
-    void* fn_wpe5;    // 5 waves/SIMD (<= 96 VGPRs), PL_TREE_WPE=5
+    void* fn_wpe5;    // unused (5 waves/SIMD spilled badly: 13 ms)
     int lds;
     int64_t ws;
 };
 
-template <int NL, int LCAP, bool SC, int F, int DL>
+template <int NL, int LCAP, bool SC, int F, int DL, bool VARIANTS = false>
 TreeEntry make_entry() {
     using G = TG<NL, LCAP, F, DL>;
+    void* w1 = nullptr;
+    if constexpr (VARIANTS) w1 = (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 1>;
     return TreeEntry{NL, LCAP, SC, F, DL, (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 4>,
-                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, true, 4>,
-                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 1>,
-                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 5>, G::LDS, G::WS};
+                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, true, 4>, w1, nullptr, G::LDS, G::WS};
 }
 
+// (n, list capacity) pairs built with the tree kernel: the BASELINE.json
+// configurations (N=256 SC, N=1024 SC / SCL L=8 / L=32, N=4096 SCL L=8) and the
+// fused-depth alternatives of the headline one (PL_TREE_F); polar_lane.hip
+// serves every other (N, L).
 const TreeEntry* tree_table(int* count) {
     static const TreeEntry tab[] = {
-        make_entry<10, 8, false, 3, 7>(),
+        make_entry<10, 8, false, 3, 7, true>(),
         make_entry<10, 8, false, 2, 7>(),
         make_entry<10, 8, false, 4, 7>(),
+        make_entry<10, 32, false, 3, 7>(),
+        make_entry<12, 8, false, 3, 9>(),
+        make_entry<10, 1, true, 3, 7>(),
+        make_entry<8, 1, true, 3, 5>(),
     };
     *count = (int)(sizeof(tab) / sizeof(tab[0]));
     return tab;
@@ -543,7 +551,7 @@ bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info) {
         if (t[k].n == n && t[k].lcap == lcap && t[k].sc == sc && (!want_f || t[k].F == want_f)) {
             const char* w = std::getenv("PL_TREE_WPE");
             const int wpe = w ? std::atoi(w) : 4;
-            info->fn = wpe == 1 ? t[k].fn_wpe1 : (wpe == 5 ? t[k].fn_wpe5 : t[k].fn);
+            info->fn = (wpe == 1 && t[k].fn_wpe1) ? t[k].fn_wpe1 : t[k].fn;
             info->fn_stamps = t[k].fn_stamps;
             info->lds_bytes = t[k].lds;
             info->ws_bytes = t[k].ws;

@@ -94,6 +94,15 @@ def traffic_source(name):
         return None
 
 
+def _traffic_rate(roof):
+    """Measured HBM-side bytes per launch (PMC) over the live kernel time: the
+    bandwidth the kernel actually draws, beside the algorithmic-bytes roofline."""
+    if roof.get("traffic"):
+        gbs = roof["traffic"] / (roof["kernel_ms"] / 1e3) / 1e9
+        roof["traffic_GBps"] = gbs
+        roof["traffic_frac"] = gbs / HBM_PEAK_GBS
+
+
 def cpu_threads():
     n = len(os.sched_getaffinity(0))
     return max(1, min(16, n))
@@ -140,10 +149,12 @@ def bench_polar(args, rank, world):
                              traffic_unit="HBM bytes per launch (2*FETCH_SIZE+WRITE_SIZE, rocprofv3 PMC)",
                              traffic_source=traffic_source("polar_scl_1024_l8"),
                              algorithmic_bytes_per_frame=bytes_per_frame, frames_per_launch=B,
-                             kernel="polar_lane_kernel<%d,false,%d,%d>" % (L, plan.info.fused_top,
-                                                                            min(3, 10 - plan.info.fused_top)),
+                             kernel=("polar_tree_kernel<n=10,LCAP=%d,SCL,F=%d>" % (L, plan.info.fused_top)
+                                     if plan.info.reserved == 4 else "polar_lane_kernel (generation %d)"
+                                     % plan.info.reserved),
                              kernel_ms=kms),
                plan=dict(lds_bytes=plan.info.lds_bytes, fused_top=plan.info.fused_top))
+    _traffic_rate(res["roofline"])
     c = counts.cpu().numpy()
     res["ber"] = float(c[0]) / max(1, c[2] * K)
     res["fer"] = float(c[1]) / max(1, c[2])
@@ -205,6 +216,7 @@ def bench_ldpc(args, rank, world):
                              traffic_unit="HBM bytes per launch (2*FETCH_SIZE+WRITE_SIZE, rocprofv3 PMC)",
                              traffic_source=traffic_source("ldpc_bp_504"),
                              algorithmic_bytes_per_frame=bpf, frames_per_launch=B, kernel_ms=kms))
+    _traffic_rate(res["roofline"])
     if rank == 0 and world == 1 and not args.skip_cpu:
         from oracle import oracle as O
         from polarcode_and_ldpc_amd.ldpc import dense_to_csr

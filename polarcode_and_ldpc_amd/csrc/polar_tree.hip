@@ -66,12 +66,11 @@ struct TG {
     // ---- workspace (bytes per wave)
     // staged channel depth 0 and its path-independent f-only depths 1..NS
     // (the left-most nodes): depth d as [S_d/2][FPW] f64 pairs at st_off(d)
-    static constexpr int NS = STAGE ? (F - 1 < 2 ? F - 1 : 2) : 0;
-    static constexpr int64_t W_CH_BYTES =
-        STAGE ? (int64_t)FPW * 8 * (N + (NS >= 1 ? N / 2 : 0) + (NS >= 2 ? N / 4 : 0)) : 0;
-    static constexpr int64_t st_off(int d) {
-        return (int64_t)FPW * 8 * ((d >= 1 ? N : 0) + (d >= 2 ? N / 2 : 0));
+    static constexpr int NS = STAGE ? (F - 1 < 3 ? F - 1 : 3) : 0;
+    static constexpr int64_t st_off(int d) {  // sum_{k<d} N/2^k values
+        return (int64_t)FPW * 8 * (2 * N - (2 * N >> d));
     }
+    static constexpr int64_t W_CH_BYTES = STAGE ? st_off(NS + 1) : 0;
     static constexpr int64_t W_LLR = W_CH_BYTES;                               // pools F..DL-1
     static constexpr int64_t W_LLR_BYTES = 1024LL * ((1LL << (n - F)) - (1LL << (n - DL)));
     static constexpr int64_t W_BL = W_LLR + W_LLR_BYTES;  // beta depths 1..NB: [W_d][64] u32
@@ -237,6 +236,9 @@ PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, in
         bsrc[d] = reinterpret_cast<const uint32_t*>(ws + G::bl_off(d <= G::NB ? d : 1)) + base + field(brow, d);
         bw[d] = (d > G::NB) ? beta_get<n>(d, bb, bw5) : 0u;
     }
+    if constexpr (G::NS >= 3) {
+        if (!right[1] && !right[2] && !right[3]) return fused_loop<G, 3>(smem, ws, lane, fw, ch, right, bsrc, bw);
+    }
     if constexpr (G::NS >= 2) {
         if (!right[1] && !right[2]) return fused_loop<G, 2>(smem, ws, lane, fw, ch, right, bsrc, bw);
     }
@@ -294,30 +296,30 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         const double* __restrict__ ch = llr + (live ? frame : batch - 1) * ld;
         if constexpr (G::STAGE) {
             // channel rows of this wave's frames -> [N/2][FPW] pairs, plus the
-            // path-independent left-most nodes f(ch) and f(f(ch)) (depths 1, 2).
-            // Lane: frame l % FPW, 8 consecutive channel values per step.
+            // path-independent left-most f-only nodes of depths 1..NS.
+            // Lane: frame l % FPW, CV consecutive channel values per step.
             const int sf = lane % FPW;
             const int64_t fr = f0 + sf < batch ? f0 + sf : batch - 1;
             const double* row = llr + fr * ld;
-            double2* d0 = reinterpret_cast<double2*>(ws + G::st_off(0)) + sf;
-            double2* d1 = reinterpret_cast<double2*>(ws + G::st_off(1)) + sf;
-            double2* d2 = reinterpret_cast<double2*>(ws + G::st_off(2)) + sf;
-            constexpr int CPI = 64 / FPW;  // 8-value chunks per frame per step
-#pragma unroll 2
-            for (int cb = 0; cb < N / 8; cb += CPI) {
+            constexpr int CV = 2 << G::NS;    // channel values per lane per step
+            constexpr int CPI = 64 / FPW;     // chunks per frame per step
+#pragma unroll 1
+            for (int cb = 0; cb < N / CV; cb += CPI) {
                 const int cc = cb + lane / FPW;
-                double v[8];
+                double v[CV];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) v[k] = row[8 * cc + k];
+                for (int k = 0; k < CV; ++k) v[k] = row[CV * cc + k];
+                // depth d of the chunk: CV >> d values = CV >> (d+1) pairs
 #pragma unroll
-                for (int k = 0; k < 4; ++k) d0[(4 * cc + k) * FPW] = make_double2(v[2 * k], v[2 * k + 1]);
-                if constexpr (G::NS >= 1) {
-                    double u[4];
+                for (int d = 0; d <= G::NS; ++d) {
+                    double2* dst = reinterpret_cast<double2*>(ws + G::st_off(d)) + sf;
+                    const int np = CV >> (d + 1);
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) u[k] = f_ms(v[2 * k], v[2 * k + 1]);
-                    d1[(2 * cc) * FPW] = make_double2(u[0], u[1]);
-                    d1[(2 * cc + 1) * FPW] = make_double2(u[2], u[3]);
-                    if constexpr (G::NS >= 2) d2[cc * FPW] = make_double2(f_ms(u[0], u[1]), f_ms(u[2], u[3]));
+                    for (int k = 0; k < np; ++k) dst[(np * cc + k) * FPW] = make_double2(v[2 * k], v[2 * k + 1]);
+                    if (d < G::NS) {
+#pragma unroll
+                        for (int k = 0; k < np; ++k) v[k] = f_ms(v[2 * k], v[2 * k + 1]);
+                    }
                 }
             }
         }

@@ -58,6 +58,16 @@ typedef struct {
 int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_mask, int32_t list_size,
                          int32_t flags, pl_plan** out);
 
+/* CRC-aided list selection (build-defined extension: the reference stores
+ *   SCLDecoder's use_crc / crc_polynomial but never reads them, decoder.py:202-203,
+ *   259).  With crc_len > 0 the decoded path is the first one, in descending
+ *   final-metric order (ties: lower list index), whose u_hat[info bits] passes
+ *   crc_check of src/polar/utils.py:128-163 (bit-serial, MSB first, zero initial
+ *   register, generator `poly` without its x^crc_len term, e.g. CRC-8 0x1D,
+ *   CRC-16 0x1021, CRC-24 0x1864CFB); if none passes, the argmax path.
+ *   crc_len == 0 restores plain SCL.  List plans only (list_size >= 1). */
+int pl_polar_plan_set_crc(pl_plan* plan, int32_t crc_len, uint32_t poly);
+
 /* LDPC plan.  Replaces BPDecoder.__init__/_build_tanner_graph
  *   (src/ldpc/decoder.py:18-60) for algo PL_LDPC_BP and MSDecoder.__init__
  *   (:215-255) for PL_LDPC_MS.  H given as CSR over its m rows with ascending

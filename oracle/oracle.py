@@ -38,6 +38,8 @@ def lib():
         L.orc_ldpc_decode_batch.argtypes = [ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_double, P, ctypes.c_int64,
                                             ctypes.c_int64, P, P, ctypes.c_int]
+        L.orc_cascl_decode_batch.argtypes = [ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int64, ctypes.c_int64, P,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
         L.orc_crc.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
         L.orc_crc.restype = ctypes.c_uint32
         _lib = L
@@ -77,6 +79,24 @@ def sc_decode(N, frozen_bits, llr, threads=1):
 
 def scl_decode(N, L, frozen_bits, llr, threads=1):
     return polar_decode_u(N, L, frozen_bits, llr, threads)[:, _info(N, frozen_bits)].astype(np.int64)
+
+
+CRC_POLY = {"CRC-8": (8, 0x1D), "CRC-16": (16, 0x1021), "CRC-24": (24, 0x1864CFB)}  # src/polar/utils.py:99-103
+
+
+def cascl_decode(N, L, frozen_bits, llr, crc_polynomial="CRC-8", threads=1):
+    """CRC-aided SCL (build-defined extension; the reference has none): u_hat[info]
+    of the first path in descending-metric order passing crc_check, else argmax."""
+    crc_len, poly = CRC_POLY.get(crc_polynomial, CRC_POLY["CRC-8"])
+    llr = np.ascontiguousarray(np.atleast_2d(np.asarray(llr, np.float64)))
+    B = llr.shape[0]
+    mask = frozen_mask(N, frozen_bits)
+    u = np.zeros((B, N), np.uint8)
+    rc = lib().orc_cascl_decode_batch(N, int(L), _ptr(mask), _ptr(llr), B, N, _ptr(u), int(threads), crc_len,
+                                      poly & 0xFFFFFFFF)
+    if rc:
+        raise RuntimeError("oracle CA-SCL decode failed: %d" % rc)
+    return u[:, _info(N, frozen_bits)].astype(np.int64)
 
 
 def ldpc_decode(row_ptr, col_idx, n, llr, algo="bp", max_iter=20, early_stop=True, norm=1.0, threads=1):

@@ -130,7 +130,14 @@ static inline double log_likelihood(double llr, int bit) {
 
 typedef struct { double m; int p; int bit; } cand_t;
 
-int orc_scl_decode(int N, int Lsz, const uint8_t* frozen_mask, const double* llr, uint8_t* u_hat) {
+uint32_t orc_crc(const uint8_t* bits, int nbits, int crc_len, uint32_t poly);
+
+/* crc_len > 0: CRC-aided selection (build-defined extension, SURVEY.md §8f rank 2;
+ * the reference stores use_crc but never reads it, decoder.py:202-203,259): the
+ * first path, in the stable descending order of the final metrics, whose
+ * u_hat[info bits] passes crc_check (src/polar/utils.py:128-163); none -> argmax. */
+static int scl_decode_impl(int N, int Lsz, const uint8_t* frozen_mask, const double* llr, uint8_t* u_hat,
+                           int crc_len, uint32_t poly) {
     if (N < 2 || (N & (N - 1)) || Lsz < 1) return ORC_EINVAL;
     const int n = log2i(N), W = n + 1;
     const size_t per = (size_t)N * W;
@@ -225,11 +232,32 @@ int orc_scl_decode(int N, int Lsz, const uint8_t* frozen_mask, const double* llr
     /* np.argmax: first maximum */
     int best = 0;
     for (int p = 1; p < Lsz; p++) if (pm[p] > pm[best]) best = p;
+    if (crc_len > 0) {
+        int na = 0;
+        for (int p = 0; p < Lsz; p++) if (act[p]) aidx[na++] = p;
+        for (int a = 1; a < na; a++) {  /* stable sort by metric, descending */
+            const int x = aidx[a];
+            int b = a - 1;
+            while (b >= 0 && pm[aidx[b]] < pm[x]) { aidx[b + 1] = aidx[b]; b--; }
+            aidx[b + 1] = x;
+        }
+        uint8_t* msg = (uint8_t*)malloc((size_t)N);
+        for (int a = 0; a < na && msg; a++) {
+            int k = 0;
+            for (int j = 0; j < N; j++) if (!frozen_mask[j]) msg[k++] = (uint8_t)(int)PB(aidx[a], j, n);
+            if (orc_crc(msg, k, crc_len, poly) == 0) { best = aidx[a]; break; }
+        }
+        free(msg);
+    }
     for (int j = 0; j < N; j++) u_hat[j] = (uint8_t)(int)PB(best, j, n);
 #undef PL
 #undef PB
     free(Lp); free(Bp); free(oL); free(oB); free(pm); free(act); free(cand); free(aidx);
     return ORC_OK;
+}
+
+int orc_scl_decode(int N, int Lsz, const uint8_t* frozen_mask, const double* llr, uint8_t* u_hat) {
+    return scl_decode_impl(N, Lsz, frozen_mask, llr, u_hat, 0, 0);
 }
 
 /* --------------------------------------------------------------- LDPC --- */
@@ -404,6 +432,20 @@ int orc_polar_decode_batch(int N, int list_size, const uint8_t* frozen_mask, con
                                 : orc_scl_decode(N, list_size, frozen_mask, llr + b * ld, u_hat + b * N);
         err |= rc ? 1 : 0;
     }
+    (void)threads;
+    return err ? ORC_EINVAL : ORC_OK;
+}
+
+/* CA-SCL batch (see scl_decode_impl): u_hat [batch, N] */
+int orc_cascl_decode_batch(int N, int list_size, const uint8_t* frozen_mask, const double* llr, int64_t batch,
+                           int64_t ld, uint8_t* u_hat, int threads, int crc_len, uint32_t poly) {
+    int err = 0;
+#ifdef _OPENMP
+    if (threads < 1) threads = 1;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1) reduction(| : err)
+#endif
+    for (int64_t b = 0; b < batch; b++)
+        err |= scl_decode_impl(N, list_size, frozen_mask, llr + b * ld, u_hat + b * N, crc_len, poly) ? 1 : 0;
     (void)threads;
     return err ? ORC_EINVAL : ORC_OK;
 }

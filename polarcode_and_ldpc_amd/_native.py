@@ -22,7 +22,7 @@ PL_LDPC_BP, PL_LDPC_MS = 0, 1
 EXPORTS = (
     "pl_polar_plan_create", "pl_ldpc_plan_create", "pl_decode", "pl_plan_reserve", "pl_plan_get_info",
     "pl_plan_destroy", "pl_last_error", "pl_random_bits", "pl_polar_encode", "pl_awgn_llr",
-    "pl_count_errors", "pl_debug_polar_stamps",
+    "pl_count_errors", "pl_debug_polar_stamps", "pl_polar_plan_set_crc",
 )
 
 
@@ -53,6 +53,7 @@ def _load():
     L.pl_awgn_llr.argtypes = [P, I32, I64, D, ctypes.c_uint64, I64, P, I64, P]
     L.pl_count_errors.argtypes = [P, I64, P, I64, I32, I64, P, P]
     L.pl_debug_polar_stamps.argtypes = [P, P, I64, I64, P, P, P]
+    L.pl_polar_plan_set_crc.argtypes = [P, I32, ctypes.c_uint32]
     for name in EXPORTS:
         getattr(L, name).restype = ctypes.c_int if name != "pl_last_error" else ctypes.c_char_p
     return L
@@ -128,6 +129,11 @@ class Plan:
         check(lib.pl_debug_polar_stamps(self._h, ctypes.c_void_p(llr.data_ptr()), llr.shape[0], _ld(llr),
                                         _dptr(bits), _dptr(stamps), ctypes.c_void_p(_stream(stream))),
               "pl_debug_polar_stamps")
+
+    def set_crc(self, crc_len: int, poly: int):
+        """CRC-aided list selection (pl_polar_plan_set_crc); crc_len 0 = off."""
+        check(lib.pl_polar_plan_set_crc(self._h, int(crc_len), ctypes.c_uint32(int(poly) & 0xFFFFFFFF)),
+              "pl_polar_plan_set_crc")
 
     def close(self):
         if getattr(self, "_h", None):

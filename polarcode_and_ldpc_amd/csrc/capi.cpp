@@ -23,6 +23,8 @@ struct pl_plan {
     uint32_t* d_frozen_dec = nullptr;  // decode-order frozen bitmask [ceil(N/32)]
     int32_t* d_info_pos = nullptr;     // [K] ascending info indices
     int32_t* d_pos2info = nullptr;     // [N] index -> info rank or -1
+    uint32_t* d_crc_g = nullptr;       // CA-SCL: CRC contribution of x_hat bit j [N] (null = plain SCL)
+    std::vector<int32_t> h_info;       // ascending info positions (host copy)
     bool tree = false;      // v4 compile-time-geometry kernel (polar_tree.hip)
     pl::TreeInfo tinfo{};
     bool lane = false;      // lane-per-path kernel (polar_lane.hip)
@@ -92,6 +94,7 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
 
     pl_plan* p = new pl_plan();
     p->kind = 0;
+    p->h_info = info;
     p->sc = (list_size == 0);
     p->list_size = list_size;
     hipGetDevice(&p->device);
@@ -321,7 +324,7 @@ extern "C" int pl_decode(pl_plan* p, const double* llr, int64_t batch, int64_t l
             const int64_t need = (batch + p->tinfo.fpw - 1) / p->tinfo.fpw;
             const int grid = (int)(need < p->lane_grid_max ? need : p->lane_grid_max);
             hipError_t e = pl::tree_launch(p->tinfo, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, p->pg.K,
-                                           p->sc ? 1 : p->list_size, p->lane_ws, grid, nullptr, s);
+                                           p->sc ? 1 : p->list_size, p->lane_ws, grid, nullptr, p->d_crc_g, s);
             return e == hipSuccess ? PL_OK : hipfail(e, "polar decode launch");
         }
         if (p->lane) {
@@ -329,7 +332,7 @@ extern "C" int pl_decode(pl_plan* p, const double* llr, int64_t batch, int64_t l
             const int64_t need = (batch + fpw - 1) / fpw;
             const int grid = (int)(need < p->lane_grid_max ? need : p->lane_grid_max);
             hipError_t e = pl::lane_launch(p->lgeo, p->sc, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch,
-                                           p->lane_ws, grid, s);
+                                           p->lane_ws, grid, p->d_crc_g, s);
             return e == hipSuccess ? PL_OK : hipfail(e, "polar decode launch");
         }
         hipError_t e = pl::polar_launch(p->pg, p->sc, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, s);
@@ -362,7 +365,8 @@ extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batc
         const int64_t need = (batch + p->tinfo.fpw - 1) / p->tinfo.fpw;
         const int grid = (int)(need < p->lane_grid_max ? need : p->lane_grid_max);
         hipError_t e = pl::tree_launch(p->tinfo, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, p->pg.K,
-                                       p->sc ? 1 : p->list_size, p->lane_ws, grid, stamps_dev, (hipStream_t)stream);
+                                       p->sc ? 1 : p->list_size, p->lane_ws, grid, stamps_dev, p->d_crc_g,
+                                       (hipStream_t)stream);
         return e == hipSuccess ? PL_OK : hipfail(e, "polar stamps launch");
     }
     if (p->lane) return fail(PL_EUNSUPPORTED, "stamps only for the tree and group kernels");
@@ -370,6 +374,32 @@ extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batc
     hipError_t e = pl::polar_launch(p->pg, p->sc, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch,
                                     (hipStream_t)stream, stamps_dev);
     return e == hipSuccess ? PL_OK : hipfail(e, "polar stamps launch");
+}
+
+extern "C" int pl_polar_plan_set_crc(pl_plan* p, int32_t crc_len, uint32_t poly) {
+    if (!p || p->kind != 0) return fail(PL_EINVAL, "not a polar plan");
+    if (p->sc) return fail(PL_EINVAL, "CRC-aided selection needs a list decoder (list_size >= 1)");
+    if (crc_len < 0 || crc_len > 32) return fail(PL_EINVAL, "crc_len must be in [0, 32]");
+    if (!p->tree && !p->lane) return fail(PL_EUNSUPPORTED, "CRC-aided selection not built for the group kernel");
+    if (p->d_crc_g) { hipFree(p->d_crc_g); p->d_crc_g = nullptr; }
+    if (crc_len == 0) return PL_OK;
+    const int N = p->pg.N;
+    // g[j] = CRC register (src/polar/utils.py:86-125, zero initial register) of
+    // the info bits of u = e_j F^{(x)n}; u_k = 1 iff k is a bit-submask of j.
+    const uint32_t top = 1u << (crc_len - 1), mask = crc_len == 32 ? 0xFFFFFFFFu : ((1u << crc_len) - 1u);
+    std::vector<uint32_t> g((size_t)N);
+    for (int j = 0; j < N; ++j) {
+        uint32_t crc = 0;
+        for (const int32_t k : p->h_info) {
+            const uint32_t bit = ((k & j) == k) ? 1u : 0u;
+            crc ^= bit << (crc_len - 1);
+            crc = (crc & top) ? ((crc << 1) ^ poly) : (crc << 1);
+            crc &= mask;
+        }
+        g[(size_t)j] = crc;
+    }
+    hipError_t e = upload(&p->d_crc_g, g);
+    return e == hipSuccess ? PL_OK : hipfail(e, "crc table upload");
 }
 
 extern "C" int pl_plan_get_info(const pl_plan* p, pl_plan_info* info) {
@@ -392,6 +422,7 @@ extern "C" int pl_plan_destroy(pl_plan* p) {
     if (p->d_frozen_dec) hipFree(p->d_frozen_dec);
     if (p->d_info_pos) hipFree(p->d_info_pos);
     if (p->d_pos2info) hipFree(p->d_pos2info);
+    if (p->d_crc_g) hipFree(p->d_crc_g);
     if (p->d_ldpc) hipFree(p->d_ldpc);
     if (p->work) hipFree(p->work);
     if (p->lane_ws) hipFree(p->lane_ws);

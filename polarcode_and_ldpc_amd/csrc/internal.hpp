@@ -37,7 +37,7 @@ int lane_geom(int N, int K, int list_size, int F, int lds_budget, LaneGeom* g);
 hipError_t lane_prepare(const LaneGeom& g, bool sc, int* max_blocks_per_cu);
 hipError_t lane_launch(const LaneGeom& g, bool sc, const double* llr, int64_t ld, uint8_t* out,
                        const uint32_t* frozen_dec, const int32_t* info_pos, int64_t batch, unsigned char* ws,
-                       int grid, hipStream_t s);
+                       int grid, const uint32_t* crc_g, hipStream_t s);
 
 // v4 lane-per-path decoder with compile-time geometry (polar_tree.hip); built
 // for the (n, list capacity) pairs in its table, polar_lane.hip covers the rest.
@@ -52,7 +52,7 @@ bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info);
 hipError_t tree_prepare(const TreeInfo& t, int* max_blocks_per_cu);
 hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t* out, const uint32_t* frozen_dec,
                        const int32_t* info_pos, int64_t batch, int K, int Lsz, unsigned char* ws, int grid,
-                       unsigned long long* stamps, hipStream_t s);
+                       unsigned long long* stamps, const uint32_t* crc_g, hipStream_t s);
 
 int polar_lcap(int list_size);  // lane-group count (power of two) for a list size
 int polar_geom(int N, int K, int list_size, int F, PolarGeom* g);  // fills layout, returns lds bytes

@@ -68,4 +68,19 @@ PL_DEV void path_metrics_fast(double pm, double lam, bool active, double& m0, do
     if (WANT1) m1 = pm + ((lam >= 0.0) ? -lam - t : -t);
 }
 
+// CRC register of u_hat[info bits] for this lane's path, from its root partial
+// sum x_hat (u = x_hat F^{(x)n} and the bit-serial CRC of src/polar/utils.py:
+// 86-163 are both GF(2)-linear with zero initial register, so the CRC is the
+// XOR of the host table g[j] over the set bits j of x_hat).  `root` points at
+// word 0 of the lane's x_hat, consecutive words `stride` u32 apart.
+PL_DEV uint32_t crc_of_xhat(const uint32_t* root, int stride, int words, const uint32_t* __restrict__ g) {
+    uint32_t crc = 0;
+    for (int w = 0; w < words; ++w) {
+        const uint32_t x = root[w * stride];
+#pragma unroll 8
+        for (int b = 0; b < 32; ++b) crc ^= ((x >> b) & 1u) ? g[32 * w + b] : 0u;
+    }
+    return crc;
+}
+
 }  // namespace pl

@@ -181,7 +181,7 @@ template <int LCAP, bool SC, int F, int B>
 __global__ void __launch_bounds__(64)
 polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_t* __restrict__ out,
                   const uint32_t* __restrict__ frozen_dec, const int32_t* __restrict__ info_pos, int64_t batch,
-                  unsigned char* __restrict__ workspace) {
+                  unsigned char* __restrict__ workspace, const uint32_t* __restrict__ crc_g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int FPW = 64 / LCAP;
     const int lane = threadIdx.x;
@@ -358,10 +358,27 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
         // ------------------------------------------------ best path, output
         int best = 0;
         if constexpr (!SC) {
-            double bm = bperm_d(c.base, pm);
-            for (int q = 1; q < nact; ++q) {
-                const double v = bperm_d(c.base + q, pm);
-                if (v > bm) { bm = v; best = q; }
+            if (crc_g) {
+                // CRC-aided selection, as polar_tree.hip
+                __syncthreads();  // root partial sums in the workspace
+                const uint32_t crc = crc_of_xhat(walkbuf(c, root_par, 0), 64, g.cw, crc_g);
+                int rank = 0;
+                for (int q = 0; q < LCAP; ++q) {
+                    const double v = bperm_d(c.base + q, pm);
+                    if (q < nact) rank += (v > pm) | ((v == pm) & (q < slot));
+                }
+                const uint32_t key = slot >= nact ? 0xFFFFu : (uint32_t)(crc == 0u ? rank : 64 + rank);
+                uint32_t bk = bperm(c.base, key);
+                for (int q = 1; q < LCAP; ++q) {
+                    const uint32_t k = bperm(c.base + q, key);
+                    if (q < nact && k < bk) { bk = k; best = q; }
+                }
+            } else {
+                double bm = bperm_d(c.base, pm);
+                for (int q = 1; q < nact; ++q) {
+                    const double v = bperm_d(c.base + q, pm);
+                    if (v > bm) { bm = v; best = q; }
+                }
             }
         }
         uint32_t* X = reinterpret_cast<uint32_t*>(smem + g.lds_final) + fw * g.cw;
@@ -475,12 +492,12 @@ hipError_t lane_prepare(const LaneGeom& g, bool sc, int* max_blocks_per_cu) {
 
 hipError_t lane_launch(const LaneGeom& g, bool sc, const double* llr, int64_t ld, uint8_t* out,
                        const uint32_t* frozen_dec, const int32_t* info_pos, int64_t batch, unsigned char* ws,
-                       int grid, hipStream_t s) {
+                       int grid, const uint32_t* crc_g, hipStream_t s) {
     void* k = lane_kernel(g, sc);
     if (!k) return hipErrorInvalidValue;
     LaneGeom gg = g;
     void* args[] = {&gg, (void*)&llr, (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos, (void*)&batch,
-                    (void*)&ws};
+                    (void*)&ws, (void*)&crc_g};
     return hipLaunchKernel(k, dim3((unsigned)grid), dim3(64), args, g.lds_bytes, s);
 }
 

@@ -265,7 +265,8 @@ template <int NL, int LCAP, bool SC, int F, int DL, bool STAMPS, int WPE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restrict__ out,
                   const uint32_t* __restrict__ frozen_dec, const int32_t* __restrict__ info_pos, int64_t batch,
-                  int K, int Lsz, unsigned char* __restrict__ workspace, unsigned long long* __restrict__ stamps) {
+                  int K, int Lsz, unsigned char* __restrict__ workspace, unsigned long long* __restrict__ stamps,
+                  const uint32_t* __restrict__ crc_g) {
     using G = TG<NL, LCAP, F, DL>;
     constexpr int n = G::n, N = G::N, FPW = G::FPW;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -465,10 +466,29 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         if constexpr (!SC) {
             met[slot] = make_double2(pm, 0.0);
             lds_sync();
-            double bm = met[0].x;
-            for (int q = 1; q < nact; ++q) {
-                const double v = met[q].x;
-                if (v > bm) { bm = v; best = q; }
+            if (crc_g) {
+                // CRC-aided selection (build-defined extension): the
+                // first path in descending-metric order (ties: lower slot) whose
+                // u_hat[info] passes the CRC; none -> that order's first = argmax
+                const uint32_t crc = crc_of_xhat(walk + root_par * G::CW * 64, 64, G::CW, crc_g);
+                int rank = 0;
+                for (int q = 0; q < nact; ++q) {
+                    const double v = met[q].x;
+                    rank += (v > pm) | ((v == pm) & (q < slot));
+                }
+                surv[slot] = slot >= nact ? 0xFFFFu : (uint32_t)(crc == 0u ? rank : 64 + rank);
+                lds_sync();
+                uint32_t bk = surv[0];
+                for (int q = 1; q < nact; ++q) {
+                    const uint32_t k = surv[q];
+                    if (k < bk) { bk = k; best = q; }
+                }
+            } else {
+                double bm = met[0].x;
+                for (int q = 1; q < nact; ++q) {
+                    const double v = met[q].x;
+                    if (v > bm) { bm = v; best = q; }
+                }
             }
             lds_sync();
         }
@@ -579,9 +599,9 @@ hipError_t tree_prepare(const TreeInfo& t, int* max_blocks_per_cu) {
 
 hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t* out, const uint32_t* frozen_dec,
                        const int32_t* info_pos, int64_t batch, int K, int Lsz, unsigned char* ws, int grid,
-                       unsigned long long* stamps, hipStream_t s) {
+                       unsigned long long* stamps, const uint32_t* crc_g, hipStream_t s) {
     void* args[] = {(void*)&llr, (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos, (void*)&batch,
-                    (void*)&K, (void*)&Lsz, (void*)&ws, (void*)&stamps};
+                    (void*)&K, (void*)&Lsz, (void*)&ws, (void*)&stamps, (void*)&crc_g};
     return hipLaunchKernel(stamps ? t.fn_stamps : t.fn, dim3((unsigned)grid), dim3(64), args, t.lds_bytes, s);
 }
 

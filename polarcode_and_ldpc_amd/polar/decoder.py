@@ -106,3 +106,27 @@ class SCLDecoder(_PolarBase):
 
     def __repr__(self) -> str:
         return f"SCLDecoder(N={self.N}, K={self.K}, L={self.L}, use_crc={self.use_crc})"
+
+
+class CASCLDecoder(SCLDecoder):
+    """CRC-aided SCL (build-defined extension; the
+    reference's SCLDecoder stores use_crc but never applies it).
+
+    The list is decoded exactly as SCLDecoder; the output is the first path, in
+    descending final-metric order (ties: lower list index), whose u_hat[info]
+    passes crc_check (src/polar/utils.py:128-163); if none does, the argmax path
+    (= SCLDecoder's answer).  The K information bits carry the message followed
+    by its CRC, as PolarEncoder(use_crc=True) lays them out (encoder.py:74-78)."""
+
+    def __init__(self, N: int, K: int, list_size: int = 8, frozen_bits: Optional[np.ndarray] = None,
+                 crc_polynomial: str = "CRC-8"):
+        super().__init__(N, K, list_size, frozen_bits, use_crc=True, crc_polynomial=crc_polynomial)
+        from .utils import CRC_POLYNOMIALS
+        name = crc_polynomial if crc_polynomial in CRC_POLYNOMIALS else "CRC-8"  # utils.py:104-105
+        self.crc_len = int(name.split("-")[1])
+        assert K > self.crc_len, f"K must be greater than CRC length ({self.crc_len})"
+        self.plan.set_crc(self.crc_len, CRC_POLYNOMIALS[name])
+
+    def __repr__(self) -> str:
+        return f"CASCLDecoder(N={self.N}, K={self.K}, L={self.L}, crc={self.crc_polynomial})"
+

@@ -220,3 +220,59 @@ def test_tree_kernel_ragged_batch(gpu):
         out = torch.empty((B, 512), dtype=torch.uint8, device="cuda")
         plan.decode(llr[:B], out)
         assert _mismatch(out.cpu().numpy(), d["scl"][:B]) == 0, B
+
+
+@pytest.mark.parametrize("N,L,crc,flags", [(1024, 32, "CRC-8", 0), (1024, 8, "CRC-16", 0), (1024, 8, "CRC-24", 0x20),
+                                           (256, 4, "CRC-8", 0), (4096, 8, "CRC-16", 0)])
+def test_cascl_vs_oracle(gpu, oracle, N, L, crc, flags):
+    """CRC-aided SCL (build-defined extension; the reference never applies its
+    CRC, so parity is against the oracle's restatement of the same rule).  Frames
+    near the waterfall so the CRC changes the pick; every frame bit-exact."""
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.polar.utils import CRC_POLYNOMIALS, crc_check, crc_encode
+    P = _P()
+    K = N // 2
+    fr = P.construct_frozen_set(N, K, 2.0)
+    clen = int(crc.split("-")[1])
+    rng = np.random.RandomState(N + L + clen)
+    B = 48 if N < 4096 else 12
+    msg = np.stack([crc_encode(rng.randint(0, 2, K - clen), crc) for _ in range(B)])
+    cw = P.PolarEncoder(N, K, frozen_bits=fr).encode_batch(msg)
+    snr = rng.uniform(0.0, 1.5, size=(B, 1))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+    llr = 2.0 * ((1.0 - 2.0 * cw) + sigma * rng.randn(B, N)) / sigma ** 2
+    want = oracle.cascl_decode(N, L, fr, llr, crc, threads=8)
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    plan = _native.polar_plan(N, K, mask, L, flags=flags)
+    plan.set_crc(clen, CRC_POLYNOMIALS[crc])
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    plan.decode(torch.from_numpy(llr).cuda(), out)
+    got = out.cpu().numpy().astype(np.int64)
+    assert _mismatch(got, want) == 0
+    # the CRC decides at least as many frames as plain SCL, and clearing it restores SCL
+    scl = oracle.scl_decode(N, L, fr, llr, threads=8)
+    assert sum(crc_check(r, crc) for r in got) >= sum(crc_check(r, crc) for r in scl)
+    plan.set_crc(0, 0)
+    plan.decode(torch.from_numpy(llr).cuda(), out)
+    assert _mismatch(out.cpu().numpy(), scl) == 0
+
+
+def test_cascl_decoder_class(gpu):
+    """CASCLDecoder drop-in: noiseless CRC'd frames round-trip; SC plans refuse CRC."""
+    from polarcode_and_ldpc_amd import _native
+    P = _P()
+    N, K = 1024, 512
+    fr = P.construct_frozen_set(N, K, 2.0)
+    enc = P.PolarEncoder(N, K, frozen_bits=fr, use_crc=True, crc_polynomial="CRC-16")
+    dec = P.CASCLDecoder(N, K, list_size=8, frozen_bits=fr, crc_polynomial="CRC-16")
+    rng = np.random.RandomState(3)
+    data = rng.randint(0, 2, (16, K - 16))
+    cw = np.stack([enc.encode(d) for d in data])
+    out = dec.decode_batch(8.0 * (1.0 - 2.0 * cw))
+    assert np.array_equal(out[:, :K - 16], data)
+    assert np.array_equal(dec.decode(8.0 * (1.0 - 2.0 * cw[0]))[:K - 16], data[0])
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    with pytest.raises(AssertionError):
+        _native.polar_plan(N, K, mask, 0).set_crc(8, 0x1D)

@@ -129,6 +129,25 @@ int pl_polar_encode(const pl_plan* plan, const uint8_t* msg_dev, int64_t batch, 
 int pl_awgn_llr(const uint8_t* codeword_dev, int32_t n, int64_t batch, double snr_db, uint64_t seed,
                 int64_t frame_offset, double* llr_dev, int64_t ld, void* stream);
 
+/* Rayleigh fading + BPSK + AWGN (src/channel/fading.py:31-63): per bit
+ * |h| (h complex Gaussian, E|h|^2 = 1), y = |h| s + N(0, sigma), LLR =
+ * 2 y |h| / sigma^2, sigma = sqrt(1/(2*10^(snr_db/10))).  Philox keyed by (seed,
+ * frame_offset + b, bit); statistically equivalent, not stream-identical. */
+int pl_rayleigh_llr(const uint8_t* codeword_dev, int32_t n, int64_t batch, double snr_db, uint64_t seed,
+                    int64_t frame_offset, double* llr_dev, int64_t ld, void* stream);
+
+/* Binary symmetric channel (src/channel/bsc.py:33-49): out[b][j] = cw[b][j] ^
+ * (u < crossover_prob), u uniform per bit; codeword_dev NULL = all-zero word. */
+int pl_bsc(const uint8_t* codeword_dev, int32_t n, int64_t batch, double crossover_prob, uint64_t seed,
+           int64_t frame_offset, uint8_t* out_dev, int64_t ld, void* stream);
+
+/* CRC append (src/polar/utils.py:86-125 crc_encode, the message layout of
+ * PolarEncoder(use_crc=True), src/polar/encoder.py:74-78): for each row b of the
+ * uint8 device matrix msg [batch][ld], writes the crc_len CRC bits of
+ * msg[b][0:k_data] (MSB first) to msg[b][k_data : k_data+crc_len]. */
+int pl_crc_append(uint8_t* msg_dev, int64_t ld, int64_t batch, int32_t k_data, int32_t crc_len, uint32_t poly,
+                  void* stream);
+
 /* Error counting (benchmarks/ber_simulation.py:180-189):
  * counts_dev[0] += bit errors, [1] += frame errors, [2] += frames, over the
  * first `width` entries of each row.  counts_dev int64[3], device. */

@@ -22,7 +22,8 @@ PL_LDPC_BP, PL_LDPC_MS = 0, 1
 EXPORTS = (
     "pl_polar_plan_create", "pl_ldpc_plan_create", "pl_decode", "pl_plan_reserve", "pl_plan_get_info",
     "pl_plan_destroy", "pl_last_error", "pl_random_bits", "pl_polar_encode", "pl_awgn_llr",
-    "pl_count_errors", "pl_debug_polar_stamps", "pl_polar_plan_set_crc",
+    "pl_count_errors", "pl_debug_polar_stamps", "pl_polar_plan_set_crc", "pl_crc_append",
+    "pl_rayleigh_llr", "pl_bsc",
 )
 
 
@@ -54,6 +55,9 @@ def _load():
     L.pl_count_errors.argtypes = [P, I64, P, I64, I32, I64, P, P]
     L.pl_debug_polar_stamps.argtypes = [P, P, I64, I64, P, P, P]
     L.pl_polar_plan_set_crc.argtypes = [P, I32, ctypes.c_uint32]
+    L.pl_crc_append.argtypes = [P, I64, I64, I32, I32, ctypes.c_uint32, P]
+    L.pl_rayleigh_llr.argtypes = [P, I32, I64, D, ctypes.c_uint64, I64, P, I64, P]
+    L.pl_bsc.argtypes = [P, I32, I64, D, ctypes.c_uint64, I64, P, I64, P]
     for name in EXPORTS:
         getattr(L, name).restype = ctypes.c_int if name != "pl_last_error" else ctypes.c_char_p
     return L
@@ -191,3 +195,23 @@ def awgn_llr(codeword: "torch.Tensor | None", n: int, batch: int, snr_db: float,
 def count_errors(ref: "torch.Tensor", dec: "torch.Tensor", width: int, counts: "torch.Tensor", stream=None):
     check(lib.pl_count_errors(_dptr(ref), _ld(ref), _dptr(dec), _ld(dec), int(width), ref.shape[0],
                               _dptr(counts), ctypes.c_void_p(_stream(stream))), "pl_count_errors")
+
+
+def crc_append(msg: "torch.Tensor", k_data: int, crc_len: int, poly: int, stream=None):
+    """msg uint8 [B, >= k_data+crc_len]: write the CRC bits of msg[:, :k_data] after them."""
+    check(lib.pl_crc_append(_dptr(msg), _ld(msg), msg.shape[0], int(k_data), int(crc_len),
+                            ctypes.c_uint32(int(poly) & 0xFFFFFFFF), ctypes.c_void_p(_stream(stream))),
+          "pl_crc_append")
+
+
+def rayleigh_llr(codeword, n: int, batch: int, snr_db: float, seed: int, frame_offset: int, llr, stream=None):
+    cw = _dptr(codeword) if codeword is not None else None
+    check(lib.pl_rayleigh_llr(cw, int(n), int(batch), float(snr_db), ctypes.c_uint64(seed & (2**64 - 1)),
+                              int(frame_offset), _dptr(llr), _ld(llr), ctypes.c_void_p(_stream(stream))),
+          "pl_rayleigh_llr")
+
+
+def bsc(codeword, n: int, batch: int, crossover_prob: float, seed: int, frame_offset: int, out, stream=None):
+    cw = _dptr(codeword) if codeword is not None else None
+    check(lib.pl_bsc(cw, int(n), int(batch), float(crossover_prob), ctypes.c_uint64(seed & (2**64 - 1)),
+                     int(frame_offset), _dptr(out), _ld(out), ctypes.c_void_p(_stream(stream))), "pl_bsc")

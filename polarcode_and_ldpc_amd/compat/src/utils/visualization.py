@@ -1,0 +1,11 @@
+"""Reference path src/utils/visualization.py -> polarcode_and_ldpc_amd.utils.visualization (import shim)."""
+import sys as _sys
+from pathlib import Path as _Path
+
+_ROOT = str(_Path(__file__).resolve().parents[4])
+if _ROOT not in _sys.path:
+    _sys.path.insert(0, _ROOT)
+
+from polarcode_and_ldpc_amd.utils.visualization import plot_ber_curves, plot_comparison, save_results  # noqa: F401
+
+__all__ = ['plot_ber_curves', 'plot_comparison', 'save_results']

@@ -455,6 +455,33 @@ extern "C" int pl_awgn_llr(const uint8_t* cw, int32_t n, int64_t batch, double s
     return e == hipSuccess ? PL_OK : hipfail(e, "awgn launch");
 }
 
+extern "C" int pl_rayleigh_llr(const uint8_t* cw, int32_t n, int64_t batch, double snr_db, uint64_t seed,
+                               int64_t frame_offset, double* llr, int64_t ld, void* stream) {
+    if (n < 1 || batch < 0 || ld < n || (!llr && batch > 0)) return fail(PL_EINVAL, "bad argument");
+    const double snr_linear = std::pow(10.0, snr_db / 10.0);  // src/channel/fading.py:21-23
+    const double sigma = std::sqrt(1.0 / (2.0 * snr_linear));
+    hipError_t e = pl::rayleigh_launch(cw, n, batch, sigma, sigma * sigma, seed, frame_offset, llr, ld,
+                                       (hipStream_t)stream);
+    return e == hipSuccess ? PL_OK : hipfail(e, "rayleigh launch");
+}
+
+extern "C" int pl_bsc(const uint8_t* cw, int32_t n, int64_t batch, double crossover_prob, uint64_t seed,
+                      int64_t frame_offset, uint8_t* out, int64_t ld, void* stream) {
+    if (n < 1 || batch < 0 || ld < n || !(crossover_prob >= 0.0 && crossover_prob <= 1.0) || (!out && batch > 0))
+        return fail(PL_EINVAL, "bad argument (crossover probability must be in [0, 1])");  // bsc.py:26
+    hipError_t e = pl::bsc_launch(cw, n, batch, crossover_prob, seed, frame_offset, out, ld, (hipStream_t)stream);
+    return e == hipSuccess ? PL_OK : hipfail(e, "bsc launch");
+}
+
+extern "C" int pl_crc_append(uint8_t* msg, int64_t ld, int64_t batch, int32_t k_data, int32_t crc_len,
+                             uint32_t poly, void* stream) {
+    if (batch < 0 || k_data < 0 || crc_len < 1 || crc_len > 32 || ld < (int64_t)k_data + crc_len ||
+        (batch > 0 && !msg))
+        return fail(PL_EINVAL, "bad argument");
+    hipError_t e = pl::crc_append_launch(msg, ld, batch, k_data, crc_len, poly, (hipStream_t)stream);
+    return e == hipSuccess ? PL_OK : hipfail(e, "crc append launch");
+}
+
 extern "C" int pl_count_errors(const uint8_t* ref, int64_t ldr, const uint8_t* dec, int64_t ldd, int32_t width,
                                int64_t batch, int64_t* counts, void* stream) {
     if (batch < 0 || width < 0 || !counts || (batch > 0 && (!ref || !dec))) return fail(PL_EINVAL, "bad argument");

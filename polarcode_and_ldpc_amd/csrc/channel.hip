@@ -92,6 +92,72 @@ __global__ void awgn_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch
     }
 }
 
+PL_DEV void normal_pair(uint64_t seed, uint32_t salt, uint32_t ctr, uint64_t f, double& z0, double& z1) {
+    const pl_u4 r = philox4x32_10(pl_u4{ctr, (uint32_t)f, (uint32_t)(f >> 32), salt}, (uint32_t)seed ^ 0x5bd1e995u,
+                                  (uint32_t)(seed >> 32));
+    const uint64_t a = ((uint64_t)r.y << 32) | r.x, c = ((uint64_t)r.w << 32) | r.z;
+    const double u1 = ((double)(a >> 11) + 1.0) * 0x1.0p-53;
+    const double u2 = (double)(c >> 11) * 0x1.0p-53;
+    const double rad = sqrt(-2.0 * log(u1));
+    double sn, cs;
+    sincospi(2.0 * u2, &sn, &cs);
+    z0 = rad * cs;
+    z1 = rad * sn;
+}
+
+// Rayleigh block-free fading (src/channel/fading.py:31-63): per bit h = |h_r + i h_i|,
+// h_r, h_i ~ N(0, 1/2); y = h s + N(0, sigma); LLR = 2 y h / sigma^2 (CSI at the
+// receiver).  One thread per bit, Philox keyed by (seed, global frame, bit).
+__global__ void rayleigh_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch, double sigma, double sigma2,
+                                uint64_t seed, int64_t off, double* __restrict__ llr, int64_t ld) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= batch * n) return;
+    const int64_t b = idx / n;
+    const int j = (int)(idx % n);
+    const uint64_t f = (uint64_t)(off + b);
+    double hr, hi, z, unused;
+    normal_pair(seed, 0xFADE0001u, (uint32_t)j, f, hr, hi);
+    normal_pair(seed, 0xFADE0002u, (uint32_t)j, f, z, unused);
+    const double h = sqrt(0.5 * (hr * hr + hi * hi));  // |h| with unit-variance components scaled by 1/sqrt(2)
+    const double s = cw ? 1.0 - 2.0 * (double)cw[b * n + j] : 1.0;
+    const double y = h * s + sigma * z;
+    llr[b * ld + j] = 2.0 * y * h / sigma2;
+}
+
+// Binary symmetric channel (src/channel/bsc.py:33-49): out = bit ^ (u < p),
+// u uniform in [0, 1) per bit.
+__global__ void bsc_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch, double p, uint64_t seed,
+                           int64_t off, uint8_t* __restrict__ out, int64_t ld) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= batch * n) return;
+    const int64_t b = idx / n;
+    const int j = (int)(idx % n);
+    const uint64_t f = (uint64_t)(off + b);
+    const pl_u4 r = philox4x32_10(pl_u4{(uint32_t)j, (uint32_t)f, (uint32_t)(f >> 32), 0xB5CB5C00u},
+                                  (uint32_t)seed ^ 0x5bd1e995u, (uint32_t)(seed >> 32));
+    const double u = (double)((((uint64_t)r.y << 32) | r.x) >> 11) * 0x1.0p-53;
+    const uint8_t bit = cw ? (uint8_t)(cw[b * n + j] & 1u) : (uint8_t)0;
+    out[b * ld + j] = bit ^ (uint8_t)(u < p ? 1 : 0);
+}
+
+hipError_t rayleigh_launch(const uint8_t* cw, int n, int64_t batch, double sigma, double sigma2, uint64_t seed,
+                           int64_t off, double* llr, int64_t ld, hipStream_t s) {
+    const int64_t tot = batch * n;
+    if (tot == 0) return hipSuccess;
+    hipLaunchKernelGGL(rayleigh_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, cw, n, batch, sigma,
+                       sigma2, seed, off, llr, ld);
+    return hipGetLastError();
+}
+
+hipError_t bsc_launch(const uint8_t* cw, int n, int64_t batch, double p, uint64_t seed, int64_t off, uint8_t* out,
+                      int64_t ld, hipStream_t s) {
+    const int64_t tot = batch * n;
+    if (tot == 0) return hipSuccess;
+    hipLaunchKernelGGL(bsc_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, cw, n, batch, p, seed, off,
+                       out, ld);
+    return hipGetLastError();
+}
+
 // one wavefront per frame; per-block partial sums -> 3 integer atomics
 __global__ void __launch_bounds__(256)
 count_errors_kernel(const uint8_t* __restrict__ ref, int64_t ldr, const uint8_t* __restrict__ dec,
@@ -142,6 +208,32 @@ hipError_t awgn_launch(const uint8_t* cw, int n, int64_t batch, double sigma, do
     if (tot == 0) return hipSuccess;
     hipLaunchKernelGGL(awgn_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, cw, n, batch, sigma,
                        sigma2, seed, off, llr, ld);
+    return hipGetLastError();
+}
+
+// CRC append (src/polar/utils.py:86-125 crc_encode, bit-serial MSB first, zero
+// initial register): msg[b][k_data + t] = bit (crc_len-1-t) of the CRC register
+// of msg[b][0:k_data].  One thread per frame (k_data sequential steps).
+__global__ void __launch_bounds__(256)
+crc_append_kernel(uint8_t* __restrict__ msg, int64_t ld, int64_t batch, int k_data, int crc_len, uint32_t poly) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    uint8_t* m = msg + b * ld;
+    const uint32_t top = 1u << (crc_len - 1), mask = crc_len == 32 ? 0xFFFFFFFFu : ((1u << crc_len) - 1u);
+    uint32_t crc = 0;
+    for (int i = 0; i < k_data; ++i) {
+        crc ^= (uint32_t)(m[i] & 1u) << (crc_len - 1);
+        crc = (crc & top) ? ((crc << 1) ^ poly) : (crc << 1);
+        crc &= mask;
+    }
+    for (int t = 0; t < crc_len; ++t) m[k_data + t] = (uint8_t)((crc >> (crc_len - 1 - t)) & 1u);
+}
+
+hipError_t crc_append_launch(uint8_t* msg, int64_t ld, int64_t batch, int k_data, int crc_len, uint32_t poly,
+                             hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    hipLaunchKernelGGL(crc_append_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, msg, ld, batch,
+                       k_data, crc_len, poly);
     return hipGetLastError();
 }
 

@@ -67,6 +67,12 @@ hipError_t random_bits_launch(uint64_t seed, int64_t off, int64_t batch, int k, 
                               hipStream_t s);
 hipError_t awgn_launch(const uint8_t* cw, int n, int64_t batch, double sigma, double sigma2,
                        uint64_t seed, int64_t off, double* llr, int64_t ld, hipStream_t s);
+hipError_t rayleigh_launch(const uint8_t* cw, int n, int64_t batch, double sigma, double sigma2, uint64_t seed,
+                           int64_t off, double* llr, int64_t ld, hipStream_t s);
+hipError_t bsc_launch(const uint8_t* cw, int n, int64_t batch, double p, uint64_t seed, int64_t off, uint8_t* out,
+                      int64_t ld, hipStream_t s);
+hipError_t crc_append_launch(uint8_t* msg, int64_t ld, int64_t batch, int k_data, int crc_len, uint32_t poly,
+                             hipStream_t s);
 hipError_t count_errors_launch(const uint8_t* ref, int64_t ldr, const uint8_t* dec, int64_t ldd,
                                int width, int64_t batch, int64_t* counts, hipStream_t s);
 

@@ -142,13 +142,12 @@ def polar_round_fn(decoder, seed: int = 0, crc_polynomial: Optional[str] = None)
         s = _stream_seed(seed, snr_index)
         if crc_polynomial is None:
             _native.random_bits(s, offset, msg)
-        else:
-            from ..polar.utils import crc_encode
-            L = int(crc_polynomial.split("-")[1])
-            data = torch.empty((nframes, K - L), dtype=torch.uint8, device="cuda")
-            _native.random_bits(s, offset, data)
-            d = data.cpu().numpy()
-            msg.copy_(torch.from_numpy(np.stack([crc_encode(r, crc_polynomial) for r in d]).astype(np.uint8)))
+        else:  # data bits + their CRC, on the device (pl_crc_append)
+            from ..polar.utils import CRC_POLYNOMIALS
+            name = crc_polynomial if crc_polynomial in CRC_POLYNOMIALS else "CRC-8"
+            L = int(name.split("-")[1])
+            _native.random_bits(s, offset, msg)
+            _native.crc_append(msg, K - L, L, CRC_POLYNOMIALS[name])
         _native.polar_encode(decoder.plan, msg, cw)
         AWGNChannel(snr_db).llr_batch_device(cw, N, nframes, seed=s ^ 0xA5A5A5A5, frame_offset=offset, out=llr)
         decoder.plan.decode(llr, out)

@@ -1,0 +1,75 @@
+"""GPU checks of the device channels, CRC append and the batched harness
+(throughput_test.py / ber_simulation.py counterparts)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_crc_append_matches_host_crc_encode(gpu):
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.polar.utils import CRC_POLYNOMIALS, crc_encode
+    for name in ("CRC-8", "CRC-16", "CRC-24"):
+        L = int(name.split("-")[1])
+        msg = torch.empty((64, 100), dtype=torch.uint8, device="cuda")
+        _native.random_bits(5, 0, msg)
+        _native.crc_append(msg, 100 - L, L, CRC_POLYNOMIALS[name])
+        m = msg.cpu().numpy().astype(int)
+        for r in m[:16]:
+            assert np.array_equal(crc_encode(r[:100 - L], name), r)
+
+
+def test_device_bsc_and_rayleigh_statistics(gpu):
+    from polarcode_and_ldpc_amd.channel import BSCChannel, RayleighFadingChannel
+    B, n = 4096, 256
+    flips = BSCChannel(0.1).transmit_batch_device(None, n, B, seed=3).double().mean().item()
+    assert abs(flips - 0.1) < 0.003
+    cw = torch.ones((B, n), dtype=torch.uint8, device="cuda")
+    again = BSCChannel(0.1).transmit_batch_device(cw, n, B, seed=3)
+    assert torch.equal(again, 1 - BSCChannel(0.1).transmit_batch_device(None, n, B, seed=3))
+    ch = RayleighFadingChannel(2.0)
+    llr = ch.llr_batch_device(None, n, B, seed=4)
+    # E[LLR | s=+1] = 2 E[|h|^2] / sigma^2 = 2 / sigma^2 with E|h|^2 = 1
+    assert abs(llr.mean().item() * ch.noise_std ** 2 / 2.0 - 1.0) < 0.01
+    # frames are independent of the batch they are generated in
+    part = ch.llr_batch_device(None, n, 8, seed=4, frame_offset=100)
+    assert torch.equal(part, llr[100:108])
+
+
+def test_throughput_harness_fields(gpu, tmp_path):
+    from polarcode_and_ldpc_amd.harness.throughput import run_throughput_test
+    r = run_throughput_test({"encoding": {"N": 256, "K": 128}},
+                            {"encoding": {"n": 504, "k": 252}, "decoding": {"max_iterations": 20}},
+                            tmp_path, num_iterations=512, snr_db=3.0)
+    saved = json.load(open(tmp_path / "data" / "throughput_results.json"))
+    for code in ("polar", "ldpc"):
+        for key in ("encoding_time", "decoding_time", "end_to_end_time", "encoding_throughput",
+                    "decoding_throughput", "end_to_end_throughput", "rate", "num_iterations"):
+            assert key in saved[code] and saved[code][key] > 0
+    assert r["ldpc"]["mean_iterations"] == 20.0  # the reference encoder's invalid codewords
+
+
+def test_ber_harness_polar_and_ldpc(gpu, tmp_path):
+    from polarcode_and_ldpc_amd.harness.ber import run_ber_simulation
+    res = run_ber_simulation(np.array([-2.0, 6.0]), num_frames=8192, max_errors=50,
+                             polar_config={"encoding": {"N": 256, "K": 128}},
+                             ldpc_config={"encoding": {"n": 504, "k": 252}, "decoding": {"max_iterations": 20}},
+                             output_dir=tmp_path, batch=4096)
+    saved = json.load(open(tmp_path / "data" / "ber_simulation_results.json"))
+    for code in ("polar", "ldpc"):
+        ber, fer = saved[code]["self"]["ber"], saved[code]["self"]["fer"]
+        assert len(ber) == 2 and ber[0] > ber[1] and fer[0] > 0.01 and fer[1] < 0.01
+        pt = saved[code]["self"]["points"][0]
+        assert pt["frame_errors"] >= 50 and pt["frames"] <= 8192  # max_errors stop, round granularity
+
+
+def test_cascl_ber_beats_scl(gpu):
+    """CA-SCL L=32 + CRC-8 (BASELINE config 4 shape) at -0.5 dB: FER below SCL's."""
+    from polarcode_and_ldpc_amd.harness.ber import simulate_polar
+    cfg = {"encoding": {"N": 1024, "K": 512}}
+    _, f_scl, _ = simulate_polar([-0.5], 8192, 10 ** 9, cfg, list_size=32, crc_polynomial=None, batch=8192)
+    _, f_ca, p = simulate_polar([-0.5], 8192, 10 ** 9, cfg, list_size=32, crc_polynomial="CRC-8", batch=8192)
+    assert p[0].frames == 8192 and f_scl[0] > 0.0 and f_ca[0] < f_scl[0]

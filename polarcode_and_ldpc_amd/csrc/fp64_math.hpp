@@ -27,6 +27,33 @@ PL_DEV double div_fast(double x, double y) {
     const double q = x * r;
     return fma(fma(-y, q, x), r, q);
 }
+// exp(-x) for x >= 0 (finite or +inf): x = k ln2 + r with |r| <= ln2/2
+// (Cody-Waite two-constant reduction), e^-r by the degree-13 Taylor polynomial
+// (truncation < 2^-57), scaled by 2^-k.  <= 1 ulp, ~19 VALU against ocml's 42.
+PL_DEV double exp_neg(double x) {
+    constexpr double INV_LN2 = 1.4426950408889634074, LN2_HI = 6.93147180369123816490e-01,
+                     LN2_LO = 1.90821492927058770002e-10;
+    const double xc = x < 746.0 ? x : 746.0;  // e^-746 underflows to 0 either way
+    const double k = __builtin_rint(xc * INV_LN2);
+    double r = fma(-k, LN2_HI, xc);
+    r = -fma(-k, LN2_LO, r);  // r = k ln2 - x, |r| <= ln2/2
+    double p = 1.6059043836821614599e-10;        // 1/13!
+    p = fma(p, r, 2.0876756987868098979e-09);    // 1/12!
+    p = fma(p, r, 2.5052108385441718775e-08);    // 1/11!
+    p = fma(p, r, 2.7557319223985890653e-07);    // 1/10!
+    p = fma(p, r, 2.7557319223985890653e-06);    // 1/9!
+    p = fma(p, r, 2.4801587301587301566e-05);    // 1/8!
+    p = fma(p, r, 1.9841269841269841253e-04);    // 1/7!
+    p = fma(p, r, 1.3888888888888888889e-03);    // 1/6!
+    p = fma(p, r, 8.3333333333333333333e-03);    // 1/5!
+    p = fma(p, r, 4.1666666666666666667e-02);    // 1/4!
+    p = fma(p, r, 1.6666666666666666667e-01);    // 1/3!
+    p = fma(p, r, 0.5);                          // 1/2!
+    p = fma(p, r, 1.0);                          // 1/1!
+    const double e = fma(p, r, 1.0);             // e^r
+    return __builtin_amdgcn_ldexp(e, -(int)k);
+}
+
 PL_DEV double lg_R(double z) {
     const double w = z * z;
     const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);

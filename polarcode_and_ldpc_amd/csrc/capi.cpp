@@ -267,9 +267,11 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     g.m = m; g.n = n; g.E = E; g.max_iter = max_iter; g.early_stop = early_stop ? 1 : 0; g.algo = algo;
     g.maxdc = maxdc; g.maxdv = maxdv; g.norm = normalization;
     g.threads = E <= 4096 ? 256 : 1024;
-    const size_t lds_all = (size_t)(2 * (size_t)E + n) * 8 + n;
+    if (E >= (1 << 20) || maxdc >= (1 << 11)) { delete p; return fail(PL_EUNSUPPORTED, "code too large"); }
+    const size_t lds_small = (size_t)8 * m + n;                 // syndrome [2][m] u32 + decisions [n]
+    const size_t lds_all = (size_t)2 * (size_t)E * 8 + lds_small;  // + T[E], C[E]
     g.use_global = lds_all > 64 * 1024 ? 1 : 0;
-    g.lds_bytes = (int)(((g.use_global ? (size_t)n : lds_all) + 15) & ~(size_t)15);
+    g.lds_bytes = (int)(((g.use_global ? lds_small : lds_all) + 15) & ~(size_t)15);
     // check-per-thread kernel (ldpc.hip ldpc_check_kernel): diagnostic, PL_LDPC_KERNEL=check
     const char* lk = std::getenv("PL_LDPC_KERNEL");
     g.check_kernel = !g.use_global && lk && std::string(lk) == "check" ? 1 : 0;
@@ -283,6 +285,12 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     all.insert(all.end(), edge_chk.begin(), edge_chk.end());
     all.insert(all.end(), var_ptr.begin(), var_ptr.end());
     all.insert(all.end(), var_edge.begin(), var_edge.end());
+    std::vector<int32_t> edge_meta(E), var_chk(E);
+    for (int k = 0; k < m; ++k)
+        for (int e = row_ptr[k]; e < row_ptr[k + 1]; ++e) edge_meta[e] = row_ptr[k] | ((row_ptr[k + 1] - row_ptr[k]) << 20);
+    for (int k = 0; k < E; ++k) var_chk[k] = edge_chk[var_edge[k]];
+    all.insert(all.end(), edge_meta.begin(), edge_meta.end());
+    all.insert(all.end(), var_chk.begin(), var_chk.end());
     hipError_t e = upload(&p->d_ldpc, all);
     if (e != hipSuccess) { pl_plan_destroy(p); return hipfail(e, "plan upload"); }
     p->ld.row_ptr = p->d_ldpc;
@@ -290,6 +298,8 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     p->ld.edge_chk = p->ld.col_idx + E;
     p->ld.var_ptr = p->ld.edge_chk + E;
     p->ld.var_edge = p->ld.var_ptr + (n + 1);
+    p->ld.edge_meta = p->ld.var_edge + E;
+    p->ld.var_chk = p->ld.edge_meta + E;
     if ((e = pl::ldpc_prepare(g)) != hipSuccess) { pl_plan_destroy(p); return hipfail(e, "hipFuncSetAttribute"); }
     *out = p;
     return PL_OK;

@@ -91,6 +91,8 @@ struct LdpcDev {
     const int32_t* edge_chk;  // [E]   edge -> check
     const int32_t* var_ptr;   // [n+1]
     const int32_t* var_edge;  // [E]   var-major list of check-major edge ids (ascending check)
+    const int32_t* edge_meta; // [E]   first edge of the edge's check | check degree << 20
+    const int32_t* var_chk;   // [E]   check of var_edge[k]
 };
 hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, int64_t ld,
                        uint8_t* bits, int32_t* iters, int64_t batch, double* work, hipStream_t s);

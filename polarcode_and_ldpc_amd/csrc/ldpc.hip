@@ -76,6 +76,20 @@ PL_DEV double np_sum_gather(const double* C, const int32_t* __restrict__ ve, int
     return res;
 }
 
+// Flooding decoder, one workgroup per frame.  State: T[E] (check inputs:
+// clip(tanh(v2c/2)) for BP, v2c for MS), C[E] (check-to-variable), bt[n]
+// (decisions), syn[2][m] (syndrome parity, double-buffered).  Per iteration:
+//   vote (early stop, it > 0): OR of the previous variable pass's syndrome
+//     parities in a __syncthreads_or -> all checks satisfied: stop with
+//     iterations = it (the reference's break after iteration it-1,
+//     decoder.py:194-198);
+//   check pass (thread = edge): C[e] = leave-one-out over the check's T in
+//     ascending neighbour order (two loops around e: the same left-to-right
+//     product as np.prod over the masked messages, decoder.py:87);
+//   variable pass (thread = variable): total = llr + np.sum(C over its checks)
+//     (NumPy pairwise order), decision total <= 0 (decoder.py:191), the next
+//     check inputs T[e] = f(total - C[e]) (v2c exactly as decoder.py:120 forms
+//     it), and the syndrome parity toggled with LDS atomics.
 template <int ALGO, bool GLOBAL, bool OCML>
 __global__ void __launch_bounds__(1024)
 ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
@@ -87,33 +101,52 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
     const int tid = threadIdx.x, nt = blockDim.x;
     const int E = g.E, n = g.n, m = g.m;
     double* T;
-    if constexpr (GLOBAL) T = work + (int64_t)blockIdx.x * (2 * (int64_t)E + n);
-    else T = reinterpret_cast<double*>(smem);
+    unsigned char* lds = smem;
+    if constexpr (GLOBAL) {
+        T = work + (int64_t)blockIdx.x * (2 * (int64_t)E);
+    } else {
+        T = reinterpret_cast<double*>(smem);
+        lds += (size_t)2 * E * sizeof(double);
+    }
     double* C = T + E;
-    double* tot = C + E;
-    uint8_t* bt = GLOBAL ? smem : reinterpret_cast<uint8_t*>(tot + n);
+    uint32_t* syn = reinterpret_cast<uint32_t*>(lds);  // [2][m]
+    uint8_t* bt = lds + (size_t)8 * m;                  // [n]
     const double* __restrict__ ch = llr + frame * ld;
+    auto tin = [&](double x) -> double {
+        if (ALGO != 0) return x;
+        return OCML ? clip999(tanh(x / 2.0)) : tanh_half_clip(x);
+    };
 
-    for (int e = tid; e < E; e += nt) C[e] = 0.0;
-    for (int v = tid; v < n; v += nt) tot[v] = ch[v];  // decoder.py:144-146 (v2c = llr)
+    for (int c = tid; c < 2 * m; c += nt) syn[c] = 0u;
+    for (int v = tid; v < n; v += nt) {  // v2c = llr (decoder.py:144-146), c2v = 0
+        const int a0 = dv.var_ptr[v], d = dv.var_ptr[v + 1] - a0;
+        const double t = tin(ch[v]);
+        for (int k = 0; k < d; ++k) {
+            const int e = dv.var_edge[a0 + k];
+            T[e] = t;
+            C[e] = 0.0;
+        }
+    }
     __syncthreads();
     int done = g.max_iter;
     for (int it = 0; it < g.max_iter; ++it) {
-        // check inputs v2c = total - c2v
-        for (int e = tid; e < E; e += nt) {
-            const double x = tot[dv.col_idx[e]] - C[e];
-            T[e] = (ALGO == 0) ? (OCML ? clip999(tanh(x / 2.0)) : tanh_half_clip(x)) : x;
+        uint32_t* sprev = syn + ((it + 1) & 1) * m;  // toggled by the previous variable pass
+        uint32_t* scur = syn + (it & 1) * m;         // toggled by this iteration's variable pass
+        if (g.early_stop && it > 0) {                // decoder.py:194-198, after iteration it-1
+            int bad = 0;
+            for (int c = tid; c < m; c += nt) bad |= (int)sprev[c];
+            if (!__syncthreads_or(bad)) { done = it; break; }
         }
-        __syncthreads();
-        // leave-one-out check outputs
+        // ---- check pass
+        for (int c = tid; c < m; c += nt) scur[c] = 0u;
         for (int e = tid; e < E; e += nt) {
-            const int c = dv.edge_chk[e];
-            const int e0 = dv.row_ptr[c], d = dv.row_ptr[c + 1] - e0, i = e - e0;
+            const int meta = dv.edge_meta[e];
+            const int e0 = meta & 0xFFFFF, d = meta >> 20, i = e - e0;
             double o;
             if (ALGO == 0) {
                 double p = 1.0;
-                for (int k = 0; k < d; ++k)
-                    if (k != i) p *= T[e0 + k];
+                for (int k = 0; k < i; ++k) p *= T[e0 + k];
+                for (int k = i + 1; k < d; ++k) p *= T[e0 + k];
                 p = clip999(p);
                 o = OCML ? 2.0 * atanh(p) : two_atanh(p);
                 if (isnan(o)) o = 0.0;
@@ -135,32 +168,24 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
             C[e] = o;
         }
         __syncthreads();
-        // variable update + hard decision (decoder.py:171-191)
+        // ---- variable pass
         for (int v = tid; v < n; v += nt) {
             const int a0 = dv.var_ptr[v], d = dv.var_ptr[v + 1] - a0;
             const double total = ch[v] + np_sum_gather(C, dv.var_edge + a0, d);
-            tot[v] = total;
-            bt[v] = total <= 0.0 ? 1 : 0;
-        }
-        if (g.early_stop) {  // decoder.py:194-198
-            __syncthreads();
-            int bad = 0;
-            for (int c = tid; c < m; c += nt) {
-                int s = 0;
-                for (int e = dv.row_ptr[c]; e < dv.row_ptr[c + 1]; ++e) s ^= bt[dv.col_idx[e]];
-                bad |= s;
+            const bool one = total <= 0.0;
+            bt[v] = one ? 1 : 0;
+            for (int k = 0; k < d; ++k) {
+                const int e = dv.var_edge[a0 + k];
+                T[e] = tin(total - C[e]);
+                if (one) atomicXor(&scur[dv.var_chk[a0 + k]], 1u);
             }
-            if (!__syncthreads_or(bad)) { done = it + 1; break; }
-        } else {
-            __syncthreads();
         }
+        __syncthreads();
     }
-    __syncthreads();
     uint8_t* o = bits + frame * (int64_t)n;
     for (int v = tid; v < n; v += nt) o[v] = bt[v];
     if (iters && tid == 0) iters[frame] = done;
 }
-
 
 // Thread-per-check kernel: one workgroup (256 threads) per frame, all state in
 // LDS: C[E] (check-to-variable), T[E] (check inputs), tot[n].  Checks are
@@ -254,7 +279,7 @@ ldpc_check_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_
 }
 
 size_t ldpc_work_bytes_per_frame(const LdpcGeom& g) {
-    return g.use_global ? (size_t)(2 * (size_t)g.E + g.n) * sizeof(double) : 0;
+    return g.use_global ? (size_t)(2 * (size_t)g.E) * sizeof(double) : 0;
 }
 
 template <int ALGO>

@@ -49,7 +49,7 @@ PL_DEV double tanh_half_clip(double x) {
     const double ax = fabs(x);
     double t = 0.999999;
     if (ax <= 30.0) {
-        const double em = expm1(-ax);
+        const double em = expm1_neg(-ax);
         t = div_fast(-em, 2.0 + em);
         t = t > 0.999999 ? 0.999999 : t;
     }

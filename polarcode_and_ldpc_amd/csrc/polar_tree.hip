@@ -545,18 +545,25 @@ TreeEntry make_entry() {
 }
 
 // (n, list capacity) pairs built with the tree kernel: the BASELINE.json
-// configurations (N=256 SC, N=1024 SC / SCL L=8 / L=32, N=4096 SCL L=8) and the
-// fused-depth alternatives of the headline one (PL_TREE_F); polar_lane.hip
-// serves every other (N, L).
+// configurations (N=256 SC, N=1024 SC / SCL L=8 / L=32, N=4096 SCL L=8), SCL
+// L=4/16 at N=1024, L=8 at N=2048, SC at N=256..4096, and the fused-depth
+// alternatives of the headline one (PL_TREE_F); polar_lane.hip serves every
+// other (N, L).
 const TreeEntry* tree_table(int* count) {
     static const TreeEntry tab[] = {
         make_entry<10, 8, false, 3, 7, true>(),
         make_entry<10, 8, false, 2, 7>(),
         make_entry<10, 8, false, 4, 7>(),
         make_entry<10, 32, false, 3, 7>(),
+        make_entry<10, 16, false, 3, 7>(),
+        make_entry<10, 4, false, 3, 7>(),
+        make_entry<11, 8, false, 3, 8>(),
         make_entry<12, 8, false, 3, 9>(),
-        make_entry<10, 1, true, 3, 7>(),
         make_entry<8, 1, true, 3, 5>(),
+        make_entry<9, 1, true, 3, 6>(),
+        make_entry<10, 1, true, 3, 7>(),
+        make_entry<11, 1, true, 3, 8>(),
+        make_entry<12, 1, true, 3, 9>(),
     };
     *count = (int)(sizeof(tab) / sizeof(tab[0]));
     return tab;

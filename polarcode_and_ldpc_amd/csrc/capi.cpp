@@ -275,6 +275,14 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     // check-per-thread kernel (ldpc.hip ldpc_check_kernel): diagnostic, PL_LDPC_KERNEL=check
     const char* lk = std::getenv("PL_LDPC_KERNEL");
     g.check_kernel = !g.use_global && lk && std::string(lk) == "check" ? 1 : 0;
+    // register-cached kernel: constant variable degree < 8, LDS-resident state
+    g.reg_variant = 0;
+    if (!g.use_global && !g.check_kernel && !(lk && std::string(lk) == "generic")) {
+        bool regular = true;
+        for (int v = 0; v < n && regular; ++v) regular = (var_ptr[v + 1] - var_ptr[v]) == maxdv;
+        if (regular && maxdv < 8) g.reg_variant = pl::ldpc_reg_variant(maxdv, E, n);
+        if (g.reg_variant) g.threads = 256;
+    }
     if (g.check_kernel) {
         g.threads = 256;
         g.lds_bytes = (int)(((size_t)(2 * (size_t)E + n) * 8 + 15) & ~(size_t)15);

@@ -84,6 +84,7 @@ struct LdpcGeom {
     int lds_bytes;     // 0 => messages live in the global workspace
     int use_global;
     int check_kernel;  // 1: ldpc_check_kernel (thread per check, state in LDS)
+    int reg_variant;   // > 0: ldpc_reg_kernel instance (constant variable degree, LDS state)
 };
 struct LdpcDev {
     const int32_t* row_ptr;   // [m+1]
@@ -98,5 +99,6 @@ hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, i
                        uint8_t* bits, int32_t* iters, int64_t batch, double* work, hipStream_t s);
 hipError_t ldpc_prepare(const LdpcGeom& g);
 size_t ldpc_work_bytes_per_frame(const LdpcGeom& g);
+int ldpc_reg_variant(int dv, int E, int n);  // 0: none fits
 
 }  // namespace pl

@@ -199,6 +199,147 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
     if (iters && tid == 0) iters[frame] = done;
 }
 
+// Register-cached variant of ldpc_decode_kernel for codes whose variable degree
+// is a constant DV < 8 (np.sum is then sequential) and whose state fits LDS:
+// 256 threads, thread tid owns edges tid + j*256 (j < EPT) and variables
+// tid + j*256 (j < VPT); their edge metadata, var_edge / var_chk lists and
+// channel LLRs are loaded once into registers instead of once per iteration.
+// Same passes, barriers and arithmetic as ldpc_decode_kernel (bit-identical).
+template <int ALGO, int DV, int EPT, int VPT>
+__global__ void __launch_bounds__(256)
+ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
+                uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int NT = 256;
+    const int64_t frame = blockIdx.x;
+    if (frame >= batch) return;
+    const int tid = threadIdx.x;
+    const int E = g.E, n = g.n, m = g.m;
+    double* T = reinterpret_cast<double*>(smem);
+    double* C = T + E;
+    uint32_t* syn = reinterpret_cast<uint32_t*>(smem + (size_t)16 * E);  // [2][m]
+    uint8_t* bt = reinterpret_cast<uint8_t*>(syn + 2 * m);               // [n]
+    const double* __restrict__ ch = llr + frame * ld;
+    auto tin = [&](double x) -> double { return ALGO == 0 ? tanh_half_clip(x) : x; };
+
+    int meta[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        const int e = tid + j * NT;
+        meta[j] = e < E ? dv.edge_meta[e] : 0;
+    }
+    int ve[VPT][DV], vc[VPT][DV];
+    double chv[VPT];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+        const int v = tid + j * NT;
+        const bool ok = v < n;
+#pragma unroll
+        for (int k = 0; k < DV; ++k) {
+            ve[j][k] = ok ? dv.var_edge[v * DV + k] : 0;
+            vc[j][k] = ok ? dv.var_chk[v * DV + k] : 0;
+        }
+        chv[j] = ok ? ch[v] : 0.0;
+    }
+    for (int c = tid; c < 2 * m; c += NT) syn[c] = 0u;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+        if (tid + j * NT < n) {
+            const double t = tin(chv[j]);
+#pragma unroll
+            for (int k = 0; k < DV; ++k) {
+                T[ve[j][k]] = t;
+                C[ve[j][k]] = 0.0;
+            }
+        }
+    }
+    __syncthreads();
+    int done = g.max_iter;
+    for (int it = 0; it < g.max_iter; ++it) {
+        uint32_t* sprev = syn + ((it + 1) & 1) * m;
+        uint32_t* scur = syn + (it & 1) * m;
+        if (g.early_stop && it > 0) {
+            int bad = 0;
+            for (int c = tid; c < m; c += NT) bad |= (int)sprev[c];
+            if (!__syncthreads_or(bad)) { done = it; break; }
+        }
+        for (int c = tid; c < m; c += NT) scur[c] = 0u;
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int e = tid + j * NT;
+            if (e >= E) break;
+            const int e0 = meta[j] & 0xFFFFF, d = meta[j] >> 20, i = e - e0;
+            double o;
+            if (ALGO == 0) {
+                double p = 1.0;
+                for (int k = 0; k < d; ++k) {
+                    const double t = T[e0 + k];
+                    p *= (k == i) ? 1.0 : t;
+                }
+                p = clip999(p);
+                o = two_atanh(p);
+                if (isnan(o)) o = 0.0;
+                else if (isinf(o)) o = o > 0.0 ? 20.0 : -20.0;
+            } else {
+                double sp = 1.0, mn = 0.0;
+                bool first = true;
+                for (int k = 0; k < d; ++k) {
+                    if (k == i) continue;
+                    const double x = T[e0 + k];
+                    sp *= np_sign(x);
+                    const double ax = fabs(x);
+                    if (first) { mn = ax; first = false; }
+                    else if (isnan(ax) || isnan(mn)) mn = __builtin_nan("");
+                    else if (ax < mn) mn = ax;
+                }
+                o = sp * mn * g.norm;
+            }
+            C[e] = o;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < VPT; ++j) {
+            const int v = tid + j * NT;
+            if (v >= n) break;
+            double sum = 0.0;  // np.sum over DV < 8 messages: sequential
+#pragma unroll
+            for (int k = 0; k < DV; ++k) sum += C[ve[j][k]];
+            const double total = chv[j] + sum;
+            const bool one = total <= 0.0;
+            bt[v] = one ? 1 : 0;
+#pragma unroll
+            for (int k = 0; k < DV; ++k) {
+                T[ve[j][k]] = tin(total - C[ve[j][k]]);
+                if (one) atomicXor(&scur[vc[j][k]], 1u);
+            }
+        }
+        __syncthreads();
+    }
+    uint8_t* o = bits + frame * (int64_t)n;
+    for (int v = tid; v < n; v += NT) o[v] = bt[v];
+    if (iters && tid == 0) iters[frame] = done;
+}
+
+// (DV, EPT, VPT) instances of ldpc_reg_kernel: E <= 256*EPT, n <= 256*VPT
+struct RegVariant { int dv, ept, vpt; void* k[2]; };
+template <int DV, int EPT, int VPT>
+static RegVariant reg_variant() {
+    return {DV, EPT, VPT, {(void*)ldpc_reg_kernel<0, DV, EPT, VPT>, (void*)ldpc_reg_kernel<1, DV, EPT, VPT>}};
+}
+static const RegVariant* reg_table(int& count) {
+    static const RegVariant t[] = {reg_variant<3, 6, 2>(), reg_variant<3, 8, 2>(), reg_variant<3, 12, 4>(),
+                                   reg_variant<3, 16, 4>(), reg_variant<4, 8, 2>(), reg_variant<4, 16, 4>()};
+    count = (int)(sizeof(t) / sizeof(t[0]));
+    return t;
+}
+int ldpc_reg_variant(int dv, int E, int n) {
+    int cnt;
+    const RegVariant* t = reg_table(cnt);
+    for (int i = 0; i < cnt; ++i)
+        if (t[i].dv == dv && E <= 256 * t[i].ept && n <= 256 * t[i].vpt) return i + 1;
+    return 0;
+}
+
 // Thread-per-check kernel: one workgroup (256 threads) per frame, all state in
 // LDS: C[E] (check-to-variable), T[E] (check inputs), tot[n].  Checks are
 // degree-sorted by the host so a wavefront's check loops have equal length.
@@ -303,6 +444,10 @@ static void* pick(bool global) {
 }
 
 static void* pick_kernel(const LdpcGeom& g) {
+    if (g.reg_variant) {
+        int cnt;
+        return reg_table(cnt)[g.reg_variant - 1].k[g.algo == 0 ? 0 : 1];
+    }
     if (g.check_kernel) return g.algo == 0 ? (void*)ldpc_check_kernel<0> : (void*)ldpc_check_kernel<1>;
     return g.algo == 0 ? pick<0>(g.use_global) : pick<1>(g.use_global);
 }

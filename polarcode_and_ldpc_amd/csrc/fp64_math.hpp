@@ -16,6 +16,21 @@ namespace pl {
 // sqrt(2), with the rounding of 1+x carried as a correction c, and log(1+f) =
 // 2s + s R(s^2), s = f/(2+f), R the published minimax fit (Lg1..Lg7, the
 // coefficients of the Sun fdlibm log kernel).
+// fma(a, b, c) as one VOP3 v_fma_f64 with all operands in VGPRs (VOP3 = true).
+// For a Horner step whose addend c is a constant the compiler otherwise emits
+// the two-address v_fmac_f64 plus a v_mov_b64 copy of the constant (2 VALU);
+// worth it in the VALU-bound LDPC kernel, harmful in the register-bound polar
+// tree kernel (the constants then occupy VGPRs), hence opt-in.
+template <bool VOP3>
+PL_DEV double fma_k(double a, double b, double c) {
+    if constexpr (VOP3) {
+        double d;
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+        return d;
+    } else {
+        return fma(a, b, c);
+    }
+}
 // x / y to <= 1 ulp: hardware reciprocal, two Newton steps, one residual step
 // (8 VALU against 13 for the IEEE-exact sequence); y finite, nonzero, normal.
 PL_DEV double div_fast(double x, double y) {
@@ -38,18 +53,18 @@ PL_DEV double exp_neg(double x) {
     double r = fma(-k, LN2_HI, xc);
     r = -fma(-k, LN2_LO, r);  // r = k ln2 - x, |r| <= ln2/2
     double p = 1.6059043836821614599e-10;        // 1/13!
-    p = fma(p, r, 2.0876756987868098979e-09);    // 1/12!
-    p = fma(p, r, 2.5052108385441718775e-08);    // 1/11!
-    p = fma(p, r, 2.7557319223985890653e-07);    // 1/10!
-    p = fma(p, r, 2.7557319223985890653e-06);    // 1/9!
-    p = fma(p, r, 2.4801587301587301566e-05);    // 1/8!
-    p = fma(p, r, 1.9841269841269841253e-04);    // 1/7!
-    p = fma(p, r, 1.3888888888888888889e-03);    // 1/6!
-    p = fma(p, r, 8.3333333333333333333e-03);    // 1/5!
-    p = fma(p, r, 4.1666666666666666667e-02);    // 1/4!
-    p = fma(p, r, 1.6666666666666666667e-01);    // 1/3!
-    p = fma(p, r, 0.5);                          // 1/2!
-    p = fma(p, r, 1.0);                          // 1/1!
+    p = fma(p, r, 2.0876756987868098979e-09);  // 1/12!
+    p = fma(p, r, 2.5052108385441718775e-08);  // 1/11!
+    p = fma(p, r, 2.7557319223985890653e-07);  // 1/10!
+    p = fma(p, r, 2.7557319223985890653e-06);  // 1/9!
+    p = fma(p, r, 2.4801587301587301566e-05);  // 1/8!
+    p = fma(p, r, 1.9841269841269841253e-04);  // 1/7!
+    p = fma(p, r, 1.3888888888888888889e-03);  // 1/6!
+    p = fma(p, r, 8.3333333333333333333e-03);  // 1/5!
+    p = fma(p, r, 4.1666666666666666667e-02);  // 1/4!
+    p = fma(p, r, 1.6666666666666666667e-01);  // 1/3!
+    p = fma(p, r, 0.5);                            // 1/2!
+    p = fma(p, r, 1.0);                            // 1/1!
     const double e = fma(p, r, 1.0);             // e^r
     return __builtin_amdgcn_ldexp(e, -(int)k);
 }
@@ -74,17 +89,18 @@ PL_DEV double expm1_neg(double x) {
     p = fma(p, r, 8.3333333333333333333e-03);
     p = fma(p, r, 4.1666666666666666667e-02);
     p = fma(p, r, 1.6666666666666666667e-01);
-    p = fma(p, r, 0.5);                          // 1/2!
+    p = fma(p, r, 0.5);                            // 1/2!
     const double em = fma(p * r, r, r);          // e^r - 1
     if (k == 0.0) return em;
     return __builtin_amdgcn_ldexp(1.0 + em, -(int)k) - 1.0;
 }
 
+template <bool VOP3 = false>
 PL_DEV double lg_R(double z) {
     const double w = z * z;
-    const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
-    const double t2 = z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01),
-                                     2.857142874366239149e-01), 6.666666666666735130e-01);
+    const double t1 = w * fma_k<VOP3>(w, fma_k<VOP3>(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
+    const double t2 = z * fma_k<VOP3>(w, fma_k<VOP3>(w, fma_k<VOP3>(w, 1.479819860511658591e-01, 1.818357216161805012e-01),
+                                         2.857142874366239149e-01), 6.666666666666735130e-01);
     return t2 + t1;
 }
 PL_DEV double log1p_pos(double x) {

@@ -48,7 +48,7 @@ PL_DEV double two_atanh(double p) {
     const double tk = __builtin_amdgcn_ldexp(1.0, k);
     const double s = div_fast(fma(a, 1.0 + tk, 1.0 - tk), fma(a, 1.0 - tk, 1.0 + tk));
     const double dk = (double)k;
-    const double r = dk * LN2_HI + ((s + s) + (s * lg_R(s * s) + dk * LN2_LO));
+    const double r = dk * LN2_HI + ((s + s) + (s * lg_R<true>(s * s) + dk * LN2_LO));
     return __builtin_isnan(p) ? p : __builtin_copysign(r, p);
 }
 // clip(tanh(x/2), +-0.999999).  e^-|x| = 2^-k e^r (Cody-Waite, |r| <= ln2/2) and
@@ -68,9 +68,9 @@ PL_DEV double tanh_half_clip(double x) {
         double r = fma(-k, LN2_HI, ax);
         r = -fma(-k, LN2_LO, r);  // k ln2 - |x|
         const double z = r * r;
-        const double Rp = z * fma(z, fma(z, fma(z, fma(z, 4.13813679705723846039e-08, -1.65339022054652515390e-06),
-                                                  6.61375632143793436117e-05), -2.77777777770155933842e-03),
-                                  1.66666666666666019037e-01);
+        const double Rp = z * fma_k<true>(z, fma_k<true>(z, fma_k<true>(z, fma_k<true>(z, 4.13813679705723846039e-08, -1.65339022054652515390e-06),
+                                                        6.61375632143793436117e-05), -2.77777777770155933842e-03),
+                                    1.66666666666666019037e-01);
         const double tk = __builtin_amdgcn_ldexp(1.0, (int)k), A = tk - 1.0, B = tk + 1.0;
         const bool big = k >= 2.0;
         const double num = big ? 2.0 * ((2.0 + r) + Rp) : fma(A, Rp, fma(-B, r, A + A));

@@ -100,6 +100,29 @@ PL_DEV double np_sum_gather(const double* C, const int32_t* __restrict__ ve, int
     return res;
 }
 
+// Min-sum check output for edge i of a degree-d check (decoder.py:270-287):
+// (prod_{k != i} np.sign(x_k)) * min_{k != i} |x_k| * normalization.  The
+// sequential sign product is +-1 by the parity of negatives, +-0 (same parity)
+// if any factor is zero (np.sign(+-0) = +0), NaN if any is NaN; the min is
+// NaN-propagating like np.min.  Same value as the loop it restates.
+PL_DEV double ms_check(const double* x, int i, int d, double norm) {
+    const double* hi = x + 1;
+    double mn = 0.0;
+    uint32_t neg = 0, zero = 0, nan = 0;
+    for (int k = 0; k < d - 1; ++k) {
+        const double v = (k < i ? x : hi)[k];
+        neg ^= v < 0.0 ? 1u : 0u;
+        zero |= v == 0.0 ? 1u : 0u;
+        nan |= __builtin_isnan(v) ? 1u : 0u;
+        const double av = fabs(v);
+        mn = (k == 0 || av < mn) ? av : mn;
+    }
+    double sp = neg ? -1.0 : 1.0;
+    sp = zero ? sp * 0.0 : sp;
+    sp = nan ? __builtin_nan("") : sp;
+    return sp * mn * norm;
+}
+
 // Flooding decoder, one workgroup per frame.  State: T[E] (check inputs:
 // clip(tanh(v2c/2)) for BP, v2c for MS), C[E] (check-to-variable), bt[n]
 // (decisions), syn[2][m] (syndrome parity, double-buffered).  Per iteration:
@@ -168,30 +191,18 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
             const int e0 = meta & 0xFFFFF, d = meta >> 20, i = e - e0;
             double o;
             if (ALGO == 0) {
-                // np.prod over the masked messages, left to right; the own
-                // message enters as an exact 1.0 so the loop is lane-uniform
+                // np.prod over the masked messages, left to right (see ldpc_reg_kernel)
+                const double* lo = T + e0;
+                const double* hi = lo + 1;
                 double p = 1.0;
-                for (int k = 0; k < d; ++k) {
-                    const double t = T[e0 + k];
-                    p *= (k == i) ? 1.0 : t;
-                }
-                p = clip999(p);
+#pragma unroll 4
+                for (int k = 0; k < d - 1; ++k) p *= (k < i ? lo : hi)[k];
+                const bool pn = __builtin_isnan(p);
+                p = __builtin_fmax(__builtin_fmin(p, 0.999999), -0.999999);
                 o = OCML ? 2.0 * atanh(p) : two_atanh(p);
-                if (isnan(o)) o = 0.0;
-                else if (isinf(o)) o = o > 0.0 ? 20.0 : -20.0;
+                o = pn ? 0.0 : o;  // nan_to_num; 2*atanh is finite after the clip
             } else {
-                double sp = 1.0, mn = 0.0;
-                bool first = true;
-                for (int k = 0; k < d; ++k) {
-                    if (k == i) continue;
-                    const double x = T[e0 + k];
-                    sp *= np_sign(x);
-                    const double ax = fabs(x);
-                    if (first) { mn = ax; first = false; }
-                    else if (isnan(ax) || isnan(mn)) mn = __builtin_nan("");
-                    else if (ax < mn) mn = ax;
-                }
-                o = sp * mn * g.norm;
+                o = ms_check(T + e0, i, d, g.norm);
             }
             C[e] = o;
         }
@@ -300,18 +311,7 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
                 o = two_atanh(__builtin_fmax(__builtin_fmin(p, 0.999999), -0.999999));
                 o = pn ? 0.0 : o;
             } else {
-                double sp = 1.0, mn = 0.0;
-                bool first = true;
-                for (int k = 0; k < d; ++k) {
-                    if (k == i) continue;
-                    const double x = T[e0 + k];
-                    sp *= np_sign(x);
-                    const double ax = fabs(x);
-                    if (first) { mn = ax; first = false; }
-                    else if (isnan(ax) || isnan(mn)) mn = __builtin_nan("");
-                    else if (ax < mn) mn = ax;
-                }
-                o = sp * mn * g.norm;
+                o = ms_check(T + e0, i, d, g.norm);
             }
             C[e] = o;
         }

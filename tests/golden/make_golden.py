@@ -351,8 +351,36 @@ def job_crc():
     return "crc.npz", out
 
 
+
+
+def job_ldpc_special():
+    """NaN / +-inf / +-0 / denormal channel LLRs through the reference BP (seed-42
+    mackay H) and MS (regular H, normalization 0.75): nan_to_num of the BP check
+    output, NaN-propagating np.min, np.sign(+-0) = 0."""
+    _, ldpc, _ = _imp()
+    n, k = 504, 252
+    Hb = ldpc.LDPCEncoder(n, k, dv=3, dc=6, seed=42).H
+    Hm = regular_36_H(n, 3)
+    rng = np.random.RandomState(29)
+    B = 12
+    llr = 2.0 * (1.0 + 0.8 * rng.randn(B, n)) / 0.64
+    for f in range(B):
+        idx = rng.choice(n, size=1 + f % 6, replace=False)
+        llr[f, idx] = [np.nan, np.inf, -np.inf, 0.0, -0.0, 1e-300][: len(idx)]
+    out = dict(n=n, llr=llr)
+    for tag, H in (("bp", Hb), ("ms", Hm)):
+        rp, ci = csr_from_dense(H)
+        out[tag + "_row_ptr"], out[tag + "_col_idx"] = rp, ci
+    d = ldpc.BPDecoder(Hb, max_iter=20)
+    b, i = zip(*[d.decode(l, return_iterations=True) for l in llr])
+    out["bp_bits"], out["bp_iters"] = np.array(b), np.array(i)
+    d = ldpc.MSDecoder(Hm, max_iter=20, normalization=0.75)
+    out["ms_bits"] = np.array([d.decode(l) for l in llr])
+    return "ldpc_special.npz", out
+
+
 JOBS = [job_scl4096_l8, job_scl1024_l8, job_ms8192, job_scl1024_l32, job_bp504,
-        job_sc1024, job_ms504, job_small, job_p1, job_kat16, job_crc]
+        job_sc1024, job_ms504, job_small, job_p1, job_kat16, job_crc, job_ldpc_special]
 
 
 def _run(fn):

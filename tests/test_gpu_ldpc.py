@@ -128,3 +128,22 @@ def test_bp_lean_math_stress_vs_oracle(gpu, oracle):
     got_b, got_i = L.BPDecoder(H, 20, True).decode_batch(llr, return_iterations=True)
     assert np.array_equal(got_b, want_b)
     assert np.array_equal(got_i, want_i)
+
+
+@pytest.mark.parametrize("algo", ["bp", "ms"])
+@pytest.mark.parametrize("kernel", ["default", "generic"])
+def test_special_values_golden(gpu, algo, kernel, monkeypatch):
+    """NaN, +-inf, +-0 channel LLRs through both flooding kernels (the
+    register-cached one and the generic one, PL_LDPC_KERNEL=generic) against the
+    reference's own outputs (golden ldpc_special.npz): nan_to_num of the BP
+    check output, NaN-propagating min-sum, np.sign(+-0) = 0."""
+    if kernel == "generic":
+        monkeypatch.setenv("PL_LDPC_KERNEL", "generic")
+    L = _L()
+    d = golden("ldpc_special.npz")
+    H = L.csr_to_dense(d[algo + "_row_ptr"], d[algo + "_col_idx"], 504)
+    dec = L.BPDecoder(H, 20, True) if algo == "bp" else L.MSDecoder(H, 20, 0.75, True)
+    got_b, got_i = dec.decode_batch(d["llr"], return_iterations=True)
+    assert np.array_equal(got_b, d[algo + "_bits"])
+    if algo == "bp":
+        assert np.array_equal(got_i, d["bp_iters"])

@@ -89,6 +89,15 @@ def test_ms(oracle):
     assert np.array_equal(b, d["ms_0_75"])
 
 
+def test_ldpc_special_values(oracle):
+    """NaN / +-inf / +-0 channel LLRs (make_golden.job_ldpc_special)."""
+    d = golden("ldpc_special.npz")
+    b, i = oracle.ldpc_decode(d["bp_row_ptr"], d["bp_col_idx"], 504, d["llr"])
+    assert np.array_equal(b, d["bp_bits"]) and np.array_equal(i, d["bp_iters"])
+    b, _ = oracle.ldpc_decode(d["ms_row_ptr"], d["ms_col_idx"], 504, d["llr"], algo="ms", norm=0.75)
+    assert np.array_equal(b, d["ms_bits"])
+
+
 def test_ms_degree1_raises(oracle):
     d = golden("ldpc_bp_504.npz")
     with pytest.raises(ValueError):

@@ -215,7 +215,9 @@ def bench_ldpc(args, rank, world):
                              frac=achieved / HBM_PEAK_GBS, traffic=load_traffic("ldpc_bp_504"),
                              traffic_unit="HBM bytes per launch (2*FETCH_SIZE+WRITE_SIZE, rocprofv3 PMC)",
                              traffic_source=traffic_source("ldpc_bp_504"),
-                             algorithmic_bytes_per_frame=bpf, frames_per_launch=B, kernel_ms=kms))
+                             algorithmic_bytes_per_frame=bpf, frames_per_launch=B, kernel_ms=kms,
+                             kernel={2: "ldpc_reg_kernel<BP,DV=3>", 1: "ldpc_decode_kernel<BP>",
+                                     3: "ldpc_check_kernel<BP>"}.get(plan.info.reserved, "?")))
     _traffic_rate(res["roofline"])
     if rank == 0 and world == 1 and not args.skip_cpu:
         from oracle import oracle as O

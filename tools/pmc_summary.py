@@ -19,7 +19,7 @@ import sys
 
 KEYS = {  # bench.py traffic key -> kernel-name prefix
     "polar_scl_1024_l8": "void pl::polar_tree_kernel<10, 8, false, 3, 7, false, 4>",
-    "ldpc_bp_504": "void pl::ldpc_decode_kernel<0, false, false>",
+    "ldpc_bp_504": "void pl::ldpc_reg_kernel<0, 3, 6, 2>",
 }
 
 

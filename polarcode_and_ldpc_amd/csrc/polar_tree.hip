@@ -63,6 +63,7 @@ struct TG {
     static constexpr int L_END0 = L_SURV + 64 * 4;
     static constexpr int L_END1 = L_FINAL + FPW * CW * 4;
     static constexpr int LDS = (((L_END0 > L_END1) ? L_END0 : L_END1) + 15) & ~15;
+    static_assert(!STAGE || 2 * FPW * GS >= 1024, "metric/row scratch holds a 1 KB staging chunk");
     // ---- workspace (bytes per wave)
     // staged channel depth 0 and its path-independent f-only depths 1..NS
     // (the left-most nodes): depth d as [S_d/2][FPW] f64 pairs at st_off(d)
@@ -189,6 +190,59 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
     constexpr int n = G::n, F = G::F, SF = 1 << (n - F), W = 1 << (F - D0);
     Fold<G> st;
     st.lam = 0.0;
+    if constexpr (G::STAGE && G::LCAP >= W / 2) {
+        // De-duplicated staged reads: the staged depth is [S/2][FPW] pairs, so
+        // a 1 KB chunk (LCAP pairs of every frame of the wave) is contiguous.
+        // Each lane fetches one distinct 16-byte pair of it (instead of the
+        // frame's LCAP lanes all fetching the same pairs), parks the chunk in
+        // the metric/row scratch (idle during a descend) and every lane reads
+        // its frame's pairs back as LDS broadcasts.  Next chunk prefetched.
+        constexpr int CH = 1;  // pairs per lane per chunk (CH = 2: 7.5 ms against 7.06)
+        constexpr int PPI = W / 2, IPC = CH * G::LCAP / PPI, NCH = SF / IPC;
+        const double2* src = reinterpret_cast<const double2*>(ws + G::st_off(D0));
+        double2* stg = reinterpret_cast<double2*>(smem + G::L_MET);
+        double2 nxt[CH];
+#pragma unroll
+        for (int h = 0; h < CH; ++h) nxt[h] = src[h * 64 + lane];
+#pragma unroll 1
+        for (int c = 0; c < NCH; ++c) {
+            lds_sync();  // the previous chunk's reads are issued before the overwrite
+#pragma unroll
+            for (int h = 0; h < CH; ++h) stg[h * 64 + lane] = nxt[h];
+            if (c + 1 < NCH) {
+#pragma unroll
+                for (int h = 0; h < CH; ++h) nxt[h] = src[((c + 1) * CH + h) * 64 + lane];
+            }
+            lds_sync();
+#pragma unroll 2
+            for (int u = 0; u < IPC; ++u) {
+                const int t = c * IPC + u;
+                double v[W];
+#pragma unroll
+                for (int k = 0; k < PPI; ++k) {
+                    const double2 pr = stg[(u * PPI + k) * G::FPW + fw];
+                    v[2 * k] = pr.x;
+                    v[2 * k + 1] = pr.y;
+                }
+#pragma unroll
+                for (int d = D0 + 1; d <= F; ++d) {
+                    const int e0 = t << (F - d);
+                    const int m = 1 << (F - d);
+                    if (right[d]) {
+                        if (d <= G::NB && (e0 & 31) == 0) bw[d] = bsrc[d][(e0 >> 5) * 64];
+                        const uint32_t b = bw[d] >> (e0 & 31);
+#pragma unroll
+                        for (int k = 0; k < m; ++k) v[k] = g_op(v[2 * k], v[2 * k + 1], b >> k);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < m; ++k) v[k] = f_ms(v[2 * k], v[2 * k + 1]);
+                    }
+                }
+                fold<G, F>(st, v[0], t, smem, ws, lane);
+            }
+        }
+        return st.lam;
+    }
     const double2* src = reinterpret_cast<const double2*>(ws + G::st_off(D0)) + fw;
 #pragma unroll 2
     for (int t = 0; t < SF; ++t) {

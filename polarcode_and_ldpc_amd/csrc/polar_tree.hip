@@ -589,13 +589,13 @@ struct TreeEntry {
     int64_t ws;
 };
 
-template <int NL, int LCAP, bool SC, int F, int DL, bool VARIANTS = false>
+template <int NL, int LCAP, bool SC, int F, int DL, bool VARIANTS = false, int WPE = 4>
 TreeEntry make_entry() {
     using G = TG<NL, LCAP, F, DL>;
     void* w1 = nullptr;
     if constexpr (VARIANTS) w1 = (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 1>;
-    return TreeEntry{NL, LCAP, SC, F, DL, (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 4>,
-                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, true, 4>, w1, nullptr, G::LDS, G::WS};
+    return TreeEntry{NL, LCAP, SC, F, DL, (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, WPE>,
+                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, true, WPE>, w1, nullptr, G::LDS, G::WS};
 }
 
 // (n, list capacity) pairs built with the tree kernel: the BASELINE.json
@@ -630,8 +630,11 @@ bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info) {
     const TreeEntry* t = tree_table(&cnt);
     const char* fe = std::getenv("PL_TREE_F");  // diagnostic: pick the fused-top depth
     const int want_f = fe ? std::atoi(fe) : 0;
+    const char* de = std::getenv("PL_TREE_DL");  // diagnostic: pick the first LDS depth
+    const int want_dl = de ? std::atoi(de) : 0;
     for (int k = 0; k < cnt; ++k)
-        if (t[k].n == n && t[k].lcap == lcap && t[k].sc == sc && (!want_f || t[k].F == want_f)) {
+        if (t[k].n == n && t[k].lcap == lcap && t[k].sc == sc && (!want_f || t[k].F == want_f) &&
+            (!want_dl || t[k].DL == want_dl)) {
             const char* w = std::getenv("PL_TREE_WPE");
             const int wpe = w ? std::atoi(w) : 4;
             info->fn = (wpe == 1 && t[k].fn_wpe1) ? t[k].fn_wpe1 : t[k].fn;

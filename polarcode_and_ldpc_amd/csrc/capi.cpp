@@ -283,6 +283,17 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
         if (regular && maxdv < 8) g.reg_variant = pl::ldpc_reg_variant(maxdv, E, n);
         if (g.reg_variant) g.threads = 256;
     }
+    // min-sum codes whose T/C arrays exceed LDS: compressed check state in LDS
+    g.compact = 0;
+    if (g.use_global && algo == 1 && maxdc <= 15 && !(lk && std::string(lk) == "generic")) {
+        const size_t lds_c = (((size_t)8 * n + 15) & ~(size_t)15) + (size_t)20 * m;
+        if (lds_c <= 160 * 1024) {
+            g.compact = 1;
+            g.use_global = 0;
+            g.threads = 1024;
+            g.lds_bytes = (int)((lds_c + 15) & ~(size_t)15);
+        }
+    }
     if (g.check_kernel) {
         g.threads = 256;
         g.lds_bytes = (int)(((size_t)(2 * (size_t)E + n) * 8 + 15) & ~(size_t)15);
@@ -297,8 +308,14 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     for (int k = 0; k < m; ++k)
         for (int e = row_ptr[k]; e < row_ptr[k + 1]; ++e) edge_meta[e] = row_ptr[k] | ((row_ptr[k + 1] - row_ptr[k]) << 20);
     for (int k = 0; k < E; ++k) var_chk[k] = edge_chk[var_edge[k]];
+    std::vector<int32_t> var_cp(E);
+    for (int k = 0; k < E; ++k) {
+        const int e = var_edge[k], c = edge_chk[e];
+        var_cp[k] = (c << 4) | ((e - row_ptr[c]) & 15);
+    }
     all.insert(all.end(), edge_meta.begin(), edge_meta.end());
     all.insert(all.end(), var_chk.begin(), var_chk.end());
+    all.insert(all.end(), var_cp.begin(), var_cp.end());
     hipError_t e = upload(&p->d_ldpc, all);
     if (e != hipSuccess) { pl_plan_destroy(p); return hipfail(e, "plan upload"); }
     p->ld.row_ptr = p->d_ldpc;
@@ -308,6 +325,7 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     p->ld.var_edge = p->ld.var_ptr + (n + 1);
     p->ld.edge_meta = p->ld.var_edge + E;
     p->ld.var_chk = p->ld.edge_meta + E;
+    p->ld.var_cp = p->ld.var_chk + E;
     if ((e = pl::ldpc_prepare(g)) != hipSuccess) { pl_plan_destroy(p); return hipfail(e, "hipFuncSetAttribute"); }
     *out = p;
     return PL_OK;
@@ -431,8 +449,9 @@ extern "C" int pl_plan_get_info(const pl_plan* p, pl_plan_info* info) {
     } else {
         info->kind = 1; info->n_in = p->lg.n; info->n_out = p->lg.n; info->list_size = 0;
         info->lds_bytes = p->lg.lds_bytes; info->fused_top = 0; info->frames_per_block = 1;
-        // kernel: 2 register-cached, 1 generic (LDS or global workspace), 3 thread-per-check
-        info->reserved = p->lg.check_kernel ? 3 : (p->lg.reg_variant ? 2 : 1);
+        // kernel: 2 register-cached, 1 generic (LDS or global workspace), 3 thread-per-check,
+        // 5 min-sum with compressed check state
+        info->reserved = p->lg.compact ? 5 : (p->lg.check_kernel ? 3 : (p->lg.reg_variant ? 2 : 1));
     }
     return PL_OK;
 }

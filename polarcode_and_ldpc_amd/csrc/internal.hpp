@@ -85,6 +85,7 @@ struct LdpcGeom {
     int use_global;
     int check_kernel;  // 1: ldpc_check_kernel (thread per check, state in LDS)
     int reg_variant;   // > 0: ldpc_reg_kernel instance (constant variable degree, LDS state)
+    int compact;       // 1: ldpc_ms_compact_kernel (min-sum, compressed check state in LDS)
 };
 struct LdpcDev {
     const int32_t* row_ptr;   // [m+1]
@@ -94,6 +95,7 @@ struct LdpcDev {
     const int32_t* var_edge;  // [E]   var-major list of check-major edge ids (ascending check)
     const int32_t* edge_meta; // [E]   first edge of the edge's check | check degree << 20
     const int32_t* var_chk;   // [E]   check of var_edge[k]
+    const int32_t* var_cp;    // [E]   check << 4 | position in the check, of var_edge[k]
 };
 hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, int64_t ld,
                        uint8_t* bits, int32_t* iters, int64_t batch, double* work, hipStream_t s);

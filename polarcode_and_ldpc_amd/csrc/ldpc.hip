@@ -359,6 +359,119 @@ int ldpc_reg_variant(int dv, int E, int n) {
     return 0;
 }
 
+// ---- min-sum with compressed check state (codes whose T/C arrays exceed LDS)
+// Min-sum check outputs are determined by a few statistics of the check's
+// inputs, so instead of T[E] and C[E] (393 KB for n = 8192) the state is
+// total[n] (fp64) plus, per check, (min1, min2) and a 32-bit word:
+//   bits 0-3 idx1 (first position attaining min1), 4-5 NaN count (saturating
+//   at 2), 6-9 position of the first NaN, 10-11 zero count, 12-15 position of
+//   the first zero, 16 parity of negatives, 17-31 negative flag per position.
+// NaN inputs are left out of (min1, min2).  ms_c2v rebuilds the exact output
+// of ms_check for position i from it (same sign product, same min, same
+// multiplications), so the decoder stays bit-identical; 8n + 20m bytes of LDS
+// (144 KB at n = 8192) hold the whole state, no global workspace.
+PL_DEV double ms_c2v(double2 mm, uint32_t meta, int i, double norm) {
+    const int idx1 = (int)(meta & 15u), ncnt = (int)((meta >> 4) & 3u), nidx = (int)((meta >> 6) & 15u);
+    const int zcnt = (int)((meta >> 10) & 3u), zidx = (int)((meta >> 12) & 15u);
+    const uint32_t neg = ((meta >> 16) ^ (meta >> (17 + i))) & 1u;  // parity of negatives over k != i
+    const double mn = (i == idx1) ? mm.y : mm.x;
+    double sp = neg ? -1.0 : 1.0;
+    sp = (zcnt >= 2 || (zcnt == 1 && zidx != i)) ? sp * 0.0 : sp;
+    sp = (ncnt >= 2 || (ncnt == 1 && nidx != i)) ? __builtin_nan("") : sp;
+    return sp * mn * norm;
+}
+
+// One workgroup (1024 threads) per frame.  Per iteration: check pass (thread =
+// check: v2c_k = total[v_k] - c2v_k(old state) as decoder.py:120 forms it --
+// llr itself at iteration 0 -- new state in place, syndrome of the decisions of
+// total rides along), vote (early stop, as ldpc_check_kernel), variable pass
+// (thread = variable: total = llr + np.sum of the rebuilt c2v in the reference's
+// order).  Decisions total <= 0.
+__global__ void __launch_bounds__(1024)
+ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
+                       uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int64_t frame = blockIdx.x;
+    if (frame >= batch) return;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int n = g.n, m = g.m;
+    double* tot = reinterpret_cast<double*>(smem);
+    double2* smin = reinterpret_cast<double2*>(smem + (((size_t)8 * n + 15) & ~(size_t)15));
+    uint32_t* smeta = reinterpret_cast<uint32_t*>(smin + m);
+    const double* __restrict__ ch = llr + frame * ld;
+    const int32_t* __restrict__ rp = dv.row_ptr;
+    const int32_t* __restrict__ ci = dv.col_idx;
+    for (int v = tid; v < n; v += nt) tot[v] = ch[v];
+    __syncthreads();
+    int done = g.max_iter;
+    for (int it = 0; it < g.max_iter; ++it) {
+        int syn = 0;
+        for (int c = tid; c < m; c += nt) {
+            const int e0 = rp[c], d = rp[c + 1] - e0;
+            const double2 om = smin[c];
+            const uint32_t ometa = smeta[c];
+            double min1 = __builtin_inf(), min2 = __builtin_inf();
+            uint32_t idx1 = 0, ncnt = 0, nidx = 0, zcnt = 0, zidx = 0, par = 0, negs = 0;
+            int s = 0;
+            for (int k = 0; k < d; ++k) {
+                const double tv = tot[ci[e0 + k]];
+                s ^= (tv <= 0.0) ? 1 : 0;
+                const double x = it == 0 ? tv : tv - ms_c2v(om, ometa, k, g.norm);
+                if (__builtin_isnan(x)) {
+                    if (ncnt == 0) nidx = (uint32_t)k;
+                    ncnt = ncnt < 2 ? ncnt + 1 : 2;
+                } else {
+                    const double a = fabs(x);
+                    if (a < min1) { min2 = min1; min1 = a; idx1 = (uint32_t)k; }
+                    else if (a < min2) min2 = a;
+                }
+                if (x == 0.0) {
+                    if (zcnt == 0) zidx = (uint32_t)k;
+                    zcnt = zcnt < 2 ? zcnt + 1 : 2;
+                }
+                if (x < 0.0) { par ^= 1u; negs |= 1u << k; }
+            }
+            syn |= s;
+            smin[c] = make_double2(min1, min2);
+            smeta[c] = idx1 | (ncnt << 4) | (nidx << 6) | (zcnt << 10) | (zidx << 12) | (par << 16) | (negs << 17);
+        }
+        if (g.early_stop && it > 0) {
+            if (!__syncthreads_or(syn)) { done = it; break; }
+        } else {
+            __syncthreads();
+        }
+        for (int v = tid; v < n; v += nt) {
+            const int a0 = dv.var_ptr[v], d = dv.var_ptr[v + 1] - a0;
+            const int32_t* __restrict__ cp = dv.var_cp + a0;
+            auto c2v = [&](int k) -> double {
+                const int c = cp[k] >> 4;
+                return ms_c2v(smin[c], smeta[c], cp[k] & 15, g.norm);
+            };
+            double sum;
+            if (d < 8) {  // np.sum: sequential below 8 terms, pairwise (8 accumulators) above
+                sum = 0.0;
+                for (int k = 0; k < d; ++k) sum += c2v(k);
+            } else {
+                double r[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) r[j] = c2v(j);
+                int k = 8;
+                for (; k < d - (d % 8); k += 8) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) r[j] += c2v(k + j);
+                }
+                sum = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+                for (; k < d; ++k) sum += c2v(k);
+            }
+            tot[v] = ch[v] + sum;
+        }
+        __syncthreads();
+    }
+    uint8_t* o = bits + frame * (int64_t)n;
+    for (int v = tid; v < n; v += nt) o[v] = tot[v] <= 0.0 ? 1 : 0;
+    if (iters && tid == 0) iters[frame] = done;
+}
+
 // Thread-per-check kernel: one workgroup (256 threads) per frame, all state in
 // LDS: C[E] (check-to-variable), T[E] (check inputs), tot[n].  Checks are
 // degree-sorted by the host so a wavefront's check loops have equal length.
@@ -463,6 +576,7 @@ static void* pick(bool global) {
 }
 
 static void* pick_kernel(const LdpcGeom& g) {
+    if (g.compact) return (void*)ldpc_ms_compact_kernel;
     if (g.reg_variant) {
         int cnt;
         return reg_table(cnt)[g.reg_variant - 1].k[g.algo == 0 ? 0 : 1];

@@ -57,12 +57,45 @@ def test_ms_504(gpu):
     assert np.array_equal(b, d["bp_bits"]) and np.array_equal(i, d["bp_iters"])
 
 
-def test_ms_8192_global_workspace(gpu):
-    """n=8192 state does not fit LDS: exercises the global-workspace kernel."""
+@pytest.mark.parametrize("kernel", ["default", "generic"])
+def test_ms_8192(gpu, kernel, monkeypatch):
+    """n=8192: T/C do not fit LDS.  Default: min-sum with the compressed check
+    state in LDS (ldpc_ms_compact_kernel); generic: T/C in a global workspace."""
+    if kernel == "generic":
+        monkeypatch.setenv("PL_LDPC_KERNEL", "generic")
     d = golden("ldpc_ms_8192.npz")
     dec = _L().MSDecoder(_H(d), max_iter=20, normalization=0.75)
-    assert dec.plan.info.lds_bytes < 64 * 1024
+    if kernel == "generic":
+        assert dec.plan.info.lds_bytes < 64 * 1024 and dec.plan.info.reserved == 1
+    else:
+        assert dec.plan.info.reserved == 5
     assert np.array_equal(dec.decode_batch(d["llr"]), d["ms_0_75"])
+
+
+@pytest.mark.parametrize("norm,es", [(0.75, True), (1.0, False)])
+def test_ms_compact_vs_oracle(gpu, oracle, norm, es):
+    """The compressed-state min-sum kernel on an n=8192 code against the oracle,
+    including exact zeros, +-inf and NaN LLRs (edge cases of its statistics)."""
+    L = _L()
+    H = L.regular_construction(8192, 3, 6, seed=1)
+    rp, ci = L.dense_to_csr(H)
+    rng = np.random.RandomState(17)
+    B = 24
+    snr = rng.uniform(0.5, 2.5, size=(B, 1))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+    llr = 2.0 * (1.0 + sigma * rng.randn(B, 8192)) / sigma ** 2
+    llr[1, ::5] = 0.0
+    llr[2, ::97] = -0.0
+    llr[3, 7] = np.nan
+    llr[4, 11], llr[4, 12] = np.inf, -np.inf
+    llr[5, :3] = np.nan
+    want_b, want_i = oracle.ldpc_decode(rp, ci, 8192, llr, algo="ms", max_iter=20, early_stop=es, norm=norm,
+                                        threads=8)
+    dec = L.MSDecoder(H, 20, norm, es)
+    assert dec.plan.info.reserved == 5
+    got_b, got_i = dec.decode_batch(llr, return_iterations=True)
+    assert np.array_equal(got_b, want_b)
+    assert np.array_equal(got_i, want_i)
 
 
 def test_ms_degree1_raises_like_reference(gpu):

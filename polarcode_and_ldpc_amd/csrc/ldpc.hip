@@ -57,13 +57,13 @@ PL_DEV double two_atanh(double p) {
 //   k <= 1: ((2^k-1)R - (2^k+1)r) / ((2^k+1)R - (2^k-1)r)
 //   k >= 2: 1 - 2(R + r) / ((2^k+1)R - (2^k-1)r)   (small correction, no cancellation)
 // <= 4 ulp, 84 % correctly rounded (the expm1 form it replaces: 57 %).  For
-// |x| > 30 tanh is above the clip bound.
+// |x| > 14.52 tanh(|x|/2) exceeds the clip bound by > 1e-8 (>> any rounding).
 PL_DEV double tanh_half_clip(double x) {
     constexpr double INV_LN2 = 1.4426950408889634074, LN2_HI = 6.93147180369123816490e-01,
                      LN2_LO = 1.90821492927058770002e-10;
     const double ax = fabs(x);
     double t = 0.999999;
-    if (ax <= 30.0) {
+    if (ax <= 14.52) {
         const double k = __builtin_rint(ax * INV_LN2);
         double r = fma(-k, LN2_HI, ax);
         r = -fma(-k, LN2_LO, r);  // k ln2 - |x|

@@ -190,7 +190,9 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
     constexpr int n = G::n, F = G::F, SF = 1 << (n - F), W = 1 << (F - D0);
     Fold<G> st;
     st.lam = 0.0;
-    if constexpr (G::STAGE && G::LCAP >= W / 2) {
+    // (n <= 10: at N = 2048 / 4096, L = 8 it measured slower, 8.7 / 13.0 ms
+    // against 8.3 / 12.0)
+    if constexpr (G::STAGE && G::LCAP >= W / 2 && G::n <= 10) {
         // De-duplicated staged reads: the staged depth is [S/2][FPW] pairs, so
         // a 1 KB chunk (LCAP pairs of every frame of the wave) is contiguous.
         // Each lane fetches one distinct 16-byte pair of it (instead of the

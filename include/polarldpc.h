@@ -150,6 +150,15 @@ int pl_bsc(const uint8_t* codeword_dev, int32_t n, int64_t batch, double crossov
 int pl_crc_append(uint8_t* msg_dev, int64_t ld, int64_t batch, int32_t k_data, int32_t crc_len, uint32_t poly,
                   void* stream);
 
+/* GF(2) block encoding (LDPC valid codewords; replaces LDPCEncoder.encode,
+ * src/ldpc/encoder.py:56-95, whose direct-solving fallback :97-187 emits
+ * non-codewords for rank-deficient H): cw[b][j] = XOR_i msg[b][i] & G[i][j] for
+ * a k x n generator G given bit-packed column-wise in device memory,
+ * g_dev[w * n + j] bit i = G[32 w + i][j], w < ceil(k / 32).  msg [batch][ld_msg]
+ * and cw [batch][ld_cw] are uint8 0/1 device matrices. */
+int pl_gf2_encode(const uint32_t* g_dev, int32_t k, int32_t n, const uint8_t* msg_dev, int64_t ld_msg,
+                  int64_t batch, uint8_t* cw_dev, int64_t ld_cw, void* stream);
+
 /* Error counting (benchmarks/ber_simulation.py:180-189):
  * counts_dev[0] += bit errors, [1] += frame errors, [2] += frames, over the
  * first `width` entries of each row.  counts_dev int64[3], device. */

@@ -23,7 +23,7 @@ EXPORTS = (
     "pl_polar_plan_create", "pl_ldpc_plan_create", "pl_decode", "pl_plan_reserve", "pl_plan_get_info",
     "pl_plan_destroy", "pl_last_error", "pl_random_bits", "pl_polar_encode", "pl_awgn_llr",
     "pl_count_errors", "pl_debug_polar_stamps", "pl_polar_plan_set_crc", "pl_crc_append",
-    "pl_rayleigh_llr", "pl_bsc",
+    "pl_rayleigh_llr", "pl_bsc", "pl_gf2_encode",
 )
 
 
@@ -58,6 +58,7 @@ def _load():
     L.pl_crc_append.argtypes = [P, I64, I64, I32, I32, ctypes.c_uint32, P]
     L.pl_rayleigh_llr.argtypes = [P, I32, I64, D, ctypes.c_uint64, I64, P, I64, P]
     L.pl_bsc.argtypes = [P, I32, I64, D, ctypes.c_uint64, I64, P, I64, P]
+    L.pl_gf2_encode.argtypes = [P, I32, I32, P, I64, I64, P, I64, P]
     for name in EXPORTS:
         getattr(L, name).restype = ctypes.c_int if name != "pl_last_error" else ctypes.c_char_p
     return L
@@ -215,3 +216,21 @@ def bsc(codeword, n: int, batch: int, crossover_prob: float, seed: int, frame_of
     cw = _dptr(codeword) if codeword is not None else None
     check(lib.pl_bsc(cw, int(n), int(batch), float(crossover_prob), ctypes.c_uint64(seed & (2**64 - 1)),
                      int(frame_offset), _dptr(out), _ld(out), ctypes.c_void_p(_stream(stream))), "pl_bsc")
+
+
+def gf2_encode(g_packed: "torch.Tensor", k: int, n: int, msg: "torch.Tensor", cw: "torch.Tensor", stream=None):
+    """cw = msg . G (GF(2)); g_packed int32 [ceil(k/32), n] device (pack_gf2_columns)."""
+    assert g_packed.dtype == torch.int32 and g_packed.is_contiguous() and g_packed.shape == ((k + 31) // 32, n)
+    check(lib.pl_gf2_encode(_dptr(g_packed), int(k), int(n), _dptr(msg), _ld(msg), msg.shape[0], _dptr(cw), _ld(cw),
+                            ctypes.c_void_p(_stream(stream))), "pl_gf2_encode")
+
+
+def pack_gf2_columns(G: np.ndarray) -> np.ndarray:
+    """k x n 0/1 matrix -> int32 [ceil(k/32), n]: bit i of [w, j] = G[32 w + i, j]."""
+    G = (np.asarray(G) & 1).astype(np.uint64)
+    k, n = G.shape
+    kw = (k + 31) // 32
+    Gp = np.zeros((kw * 32, n), np.uint64)
+    Gp[:k] = G
+    w = (Gp.reshape(kw, 32, n) << np.arange(32, dtype=np.uint64)[None, :, None]).sum(axis=1)
+    return w.astype(np.uint32).view(np.int32)

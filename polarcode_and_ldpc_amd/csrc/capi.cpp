@@ -521,6 +521,14 @@ extern "C" int pl_crc_append(uint8_t* msg, int64_t ld, int64_t batch, int32_t k_
     return e == hipSuccess ? PL_OK : hipfail(e, "crc append launch");
 }
 
+extern "C" int pl_gf2_encode(const uint32_t* g_dev, int32_t k, int32_t n, const uint8_t* msg, int64_t ld_msg,
+                             int64_t batch, uint8_t* cw, int64_t ld_cw, void* stream) {
+    if (batch < 0 || k < 1 || n < 1 || ld_msg < k || ld_cw < n || (batch > 0 && (!g_dev || !msg || !cw)))
+        return fail(PL_EINVAL, "bad argument");
+    hipError_t e = pl::gf2_encode_launch(g_dev, k, n, msg, ld_msg, batch, cw, ld_cw, (hipStream_t)stream);
+    return e == hipSuccess ? PL_OK : hipfail(e, "gf2 encode launch");
+}
+
 extern "C" int pl_count_errors(const uint8_t* ref, int64_t ldr, const uint8_t* dec, int64_t ldd, int32_t width,
                                int64_t batch, int64_t* counts, void* stream) {
     if (batch < 0 || width < 0 || !counts || (batch > 0 && (!ref || !dec))) return fail(PL_EINVAL, "bad argument");

@@ -62,6 +62,40 @@ polar_encode_kernel(int N, int K, const int32_t* __restrict__ pos2info, const ui
     for (int j = lane; j < N; j += 64) o[j] = (X[j >> 5] >> (j & 31)) & 1u;
 }
 
+// GF(2) block encoder (LDPC valid-codeword encoding, SURVEY §8 f row 3; the
+// reference's LDPCEncoder.encode, src/ldpc/encoder.py:56-95, with a generator
+// whose rows really span the code): cw[b][j] = parity(msg[b] . G[:, j]).  G is
+// bit-packed column-wise as g[w][j] (bit i of word w of column j = G[32w+i][j]),
+// so lanes taking consecutive columns read consecutive words.  One wave per
+// frame: the message is packed into LDS words by ballots, then each lane XORs
+// popcounts over the kw words of its columns.
+__global__ void __launch_bounds__(64)
+gf2_encode_kernel(const uint32_t* __restrict__ g, int k, int n, const uint8_t* __restrict__ msg, int64_t ldm,
+                  int64_t batch, uint8_t* __restrict__ cw, int64_t ldc) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* mw = reinterpret_cast<uint32_t*>(smem);
+    const int64_t b = blockIdx.x;
+    if (b >= batch) return;
+    const int lane = threadIdx.x;
+    const int kw = (k + 31) / 32;
+    const uint8_t* m = msg + b * ldm;
+    for (int base = 0; base < k; base += 64) {
+        const int j = base + lane;
+        const unsigned long long bal = __ballot(j < k ? (m[j] & 1) : 0);
+        if (lane == 0) {
+            mw[base / 32] = (uint32_t)bal;
+            if (base / 32 + 1 < kw) mw[base / 32 + 1] = (uint32_t)(bal >> 32);
+        }
+    }
+    __syncthreads();
+    uint8_t* o = cw + b * ldc;
+    for (int j = lane; j < n; j += 64) {
+        uint32_t acc = 0;
+        for (int w = 0; w < kw; ++w) acc ^= (uint32_t)__popc(mw[w] & g[(int64_t)w * n + j]);
+        o[j] = (uint8_t)(acc & 1u);
+    }
+}
+
 // two LLRs per thread (one Philox call -> two 53-bit uniforms -> Box-Muller pair)
 __global__ void awgn_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch, double sigma,
                             double sigma2, uint64_t seed, int64_t off, double* __restrict__ llr, int64_t ld) {
@@ -199,6 +233,15 @@ hipError_t polar_encode_launch(int N, int K, const int32_t* pos2info, const uint
     const int words = N < 32 ? 1 : N / 32;
     hipLaunchKernelGGL(polar_encode_kernel, dim3((unsigned)batch), dim3(64), words * 4 + 8, s, N, K, pos2info,
                        msg, batch, cw);
+    return hipGetLastError();
+}
+
+hipError_t gf2_encode_launch(const uint32_t* g, int k, int n, const uint8_t* msg, int64_t ldm, int64_t batch,
+                             uint8_t* cw, int64_t ldc, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    const int kw = (k + 31) / 32;
+    hipLaunchKernelGGL(gf2_encode_kernel, dim3((unsigned)batch), dim3(64), (size_t)kw * 4 + 8, s, g, k, n, msg, ldm,
+                       batch, cw, ldc);
     return hipGetLastError();
 }
 

@@ -71,6 +71,8 @@ hipError_t rayleigh_launch(const uint8_t* cw, int n, int64_t batch, double sigma
                            int64_t off, double* llr, int64_t ld, hipStream_t s);
 hipError_t bsc_launch(const uint8_t* cw, int n, int64_t batch, double p, uint64_t seed, int64_t off, uint8_t* out,
                       int64_t ld, hipStream_t s);
+hipError_t gf2_encode_launch(const uint32_t* g, int k, int n, const uint8_t* msg, int64_t ldm, int64_t batch,
+                             uint8_t* cw, int64_t ldc, hipStream_t s);
 hipError_t crc_append_launch(uint8_t* msg, int64_t ld, int64_t batch, int k_data, int crc_len, uint32_t poly,
                              hipStream_t s);
 hipError_t count_errors_launch(const uint8_t* ref, int64_t ldr, const uint8_t* dec, int64_t ldd,

@@ -49,17 +49,22 @@ def simulate_polar(snr_db_range: Sequence[float], num_frames: int, max_errors: i
 
 
 def simulate_ldpc(snr_db_range: Sequence[float], num_frames: int, max_errors: int, config: Dict,
-                  batch: int = 65536, seed: int = 0, group=None):
-    """ber_simulation.py:201-293 -> (ber, fer, points)."""
+                  batch: int = 65536, seed: int = 0, group=None, random_codewords: bool = False):
+    """ber_simulation.py:201-293 -> (ber, fer, points).  random_codewords: random
+    messages encoded into valid codewords on the device (LDPCEncoder.
+    encode_batch_device) instead of the all-zero codeword."""
     import torch
     from ..ldpc.decoder import BPDecoder
+    from ..ldpc.encoder import LDPCEncoder
     from ..lib_wrappers import LDPCLibWrapper
     n, k = config["encoding"]["n"], config["encoding"]["k"]
     cons = config.get("construction", config["encoding"])
     lib = LDPCLibWrapper(n, k, dv=cons.get("dv", 3), dc=cons.get("dc", 6), seed=42)
-    dec = BPDecoder(lib.get_parity_check_matrix(), max_iter=config["decoding"].get("max_iterations", 50))
-    mc = MonteCarlo(ldpc_round_fn(dec, seed=seed, info_bits=lib.k), info_bits=lib.k, batch=batch, group=group,
-                    device=torch.device("cuda", torch.cuda.current_device()))
+    H = lib.get_parity_check_matrix()
+    dec = BPDecoder(H, max_iter=config["decoding"].get("max_iterations", 50))
+    enc = LDPCEncoder(n, lib.k, H=H) if random_codewords else None
+    mc = MonteCarlo(ldpc_round_fn(dec, seed=seed, info_bits=lib.k, encoder=enc), info_bits=lib.k, batch=batch,
+                    group=group, device=torch.device("cuda", torch.cuda.current_device()))
     pts = mc.run(snr_db_range, num_frames, max_errors)
     return np.array([p.ber for p in pts]), np.array([p.fer for p in pts]), pts
 
@@ -107,6 +112,8 @@ def main(argv=None):
     ap.add_argument("--max-errors", type=int, default=100)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--ldpc-codewords", choices=["zero", "random"], default="zero",
+                    help="LDPC frames: all-zero codeword, or random messages encoded on the device")
     a = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -120,7 +127,7 @@ def main(argv=None):
     else:
         ber, fer, pts = simulate_ldpc(snr, a.frames, a.max_errors,
                                       {"encoding": {"n": a.n, "k": a.k}, "decoding": {"max_iterations": a.max_iter}},
-                                      a.batch)
+                                      a.batch, random_codewords=a.ldpc_codewords == "random")
     if int(os.environ.get("RANK", "0")) == 0:
         res = {"code": a.code, "snr_db": snr.tolist(), "ber": ber.tolist(), "fer": fer.tolist(), "gpus": world,
                "points": [p.as_dict() for p in pts]}

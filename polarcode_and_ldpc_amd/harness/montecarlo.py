@@ -158,15 +158,24 @@ def polar_round_fn(decoder, seed: int = 0, crc_polynomial: Optional[str] = None)
     return fn
 
 
-def ldpc_round_fn(decoder, seed: int = 0, info_bits: Optional[int] = None):
-    """Round function for BPDecoder/MSDecoder on the all-zero codeword (BP and
-    min-sum are codeword-symmetric); errors are counted over the first
-    `info_bits` positions, like ber_simulation.py:265-269 (decoded[:k])."""
+def ldpc_round_fn(decoder, seed: int = 0, info_bits: Optional[int] = None, encoder=None):
+    """Round function for BPDecoder/MSDecoder.
+
+    encoder None: the all-zero codeword (BP and min-sum are codeword-symmetric);
+    errors over the first `info_bits` positions, like ber_simulation.py:265-269
+    (decoded[:k]).  encoder = an LDPCEncoder: random k-bit messages (device
+    Philox), valid codewords on the device (LDPCEncoder.encode_batch_device,
+    pl_gf2_encode), errors over the encoder's info positions -- the whole Monte
+    Carlo chain device-resident."""
     import torch
     from .. import _native
     from ..channel.awgn import AWGNChannel
     n = decoder.n
-    k = info_bits if info_bits is not None else n - decoder.m
+    if encoder is not None:
+        k = encoder.k
+        info = torch.from_numpy(np.asarray(encoder.info_positions, dtype=np.int64)).cuda()
+    else:
+        k = info_bits if info_bits is not None else n - decoder.m
     bufs = {}
 
     def fn(snr_index, snr_db, offset, nframes):
@@ -174,13 +183,22 @@ def ldpc_round_fn(decoder, seed: int = 0, info_bits: Optional[int] = None):
             bufs.update(B=nframes, llr=torch.empty((nframes, n), dtype=torch.float64, device="cuda"),
                         out=torch.empty((nframes, n), dtype=torch.uint8, device="cuda"),
                         its=torch.empty((nframes,), dtype=torch.int32, device="cuda"),
-                        zero=torch.zeros((nframes, n), dtype=torch.uint8, device="cuda"))
-        llr, out, its, zero = (bufs[x][:nframes] for x in ("llr", "out", "its", "zero"))
-        AWGNChannel(snr_db).llr_batch_device(None, n, nframes, seed=_stream_seed(seed, snr_index),
-                                             frame_offset=offset, out=llr)
-        decoder.plan.decode(llr, out, its)
+                        zero=torch.zeros((nframes, n), dtype=torch.uint8, device="cuda"),
+                        msg=torch.empty((nframes, k), dtype=torch.uint8, device="cuda"),
+                        cw=torch.empty((nframes, n), dtype=torch.uint8, device="cuda"))
+        llr, out, its, zero, msg, cw = (bufs[x][:nframes] for x in ("llr", "out", "its", "zero", "msg", "cw"))
+        s = _stream_seed(seed, snr_index)
         counts = torch.zeros(3, dtype=torch.int64, device="cuda")
-        _native.count_errors(zero, out, k, counts)
+        if encoder is None:
+            AWGNChannel(snr_db).llr_batch_device(None, n, nframes, seed=s, frame_offset=offset, out=llr)
+            decoder.plan.decode(llr, out, its)
+            _native.count_errors(zero, out, k, counts)
+        else:
+            _native.random_bits(s, offset, msg)
+            encoder.encode_batch_device(msg, out=cw)
+            AWGNChannel(snr_db).llr_batch_device(cw, n, nframes, seed=s ^ 0xA5A5A5A5, frame_offset=offset, out=llr)
+            decoder.plan.decode(llr, out, its)
+            _native.count_errors(msg, out.index_select(1, info).contiguous(), k, counts)
         return counts.cpu().numpy()
 
     return fn

@@ -1,6 +1,6 @@
 """LDPC codes: drop-in BP / Min-Sum decoders (HIP) + parity-check matrices."""
 from .decoder import BPDecoder, MSDecoder
-from .encoder import LDPCEncoder
+from .encoder import LDPCEncoder, valid_generator
 from .matrix import (calculate_girth, check_matrix_rank, create_systematic_generator, csr_to_dense, dense_to_csr,
                      generate_ldpc_matrix, gf2_systematic_pair, mackay_construction, peg_construction,
                      regular_construction)

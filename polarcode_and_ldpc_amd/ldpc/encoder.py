@@ -8,6 +8,8 @@ It is evaluated here for whole batches of messages at once (one elimination,
 vectorised back-substitution) -- giving exactly the reference's
 codewords, including the *invalid* ones it emits for the seed-42 (504, 252) H
 (SURVEY.md §0 quirk 2), which is what benchmarks/throughput_test.py decodes.
+`valid_generator` / `LDPCEncoder.encode_batch_device` add encoding into valid
+codewords on the device (pl_gf2_encode).
 """
 from __future__ import annotations
 
@@ -69,6 +71,58 @@ def _solve_gf2_batch(A: np.ndarray, B: np.ndarray) -> np.ndarray:
     return X
 
 
+def valid_generator(H: np.ndarray, k: Optional[int] = None):
+    """A generator whose rows span the code of H: (G [k, n], info [k]).
+
+    The reference's encoders (systematic G, or the direct-solving fallback for a
+    rank-deficient H2, src/ldpc/encoder.py:56-131) emit non-codewords for the
+    seed-42 (504, 252) H (rank 251, rank(H2) = 236).  Here H is brought to
+    reduced row-echelon form over GF(2) with pivots taken from the right-most
+    columns first (bit-packed rows, so n = 8192 takes seconds), the free columns
+    carry the message -- the first k of them, as far left as possible, are the
+    info positions `info` (codeword[info] = message; further free columns are
+    0) -- and every pivot bit is the parity its reduced row prescribes.  H G^T =
+    0 (mod 2) by construction.  k defaults to the code dimension n - rank(H).
+    """
+    Hb = (np.asarray(H) & 1).astype(np.uint8)
+    m, n = Hb.shape
+    nw = (n + 63) // 64
+    W = np.zeros((m, nw * 64), np.uint8)
+    W[:, :n] = Hb
+    W = np.packbits(W.reshape(m, nw, 64)[:, :, ::-1], axis=2, bitorder="big").view(">u8")[:, :, 0].astype(np.uint64)
+    # W[r, w] bit b = H[r, 64 w + b]
+    pivots = []
+    r = 0
+    for c in range(n - 1, -1, -1):
+        if r == m:
+            break
+        w, b = divmod(c, 64)
+        col = (W[r:, w] >> np.uint64(b)) & np.uint64(1)
+        nz = np.nonzero(col)[0]
+        if len(nz) == 0:
+            continue
+        p = r + int(nz[0])
+        if p != r:
+            W[[r, p]] = W[[p, r]]
+        hit = np.nonzero((W[:, w] >> np.uint64(b)) & np.uint64(1))[0]
+        hit = hit[hit != r]
+        W[hit] ^= W[r]
+        pivots.append(c)
+        r += 1
+    R = ((W[:r, :, None] >> np.arange(64, dtype=np.uint64)[None, None, :]) & np.uint64(1)).astype(np.uint8)
+    R = R.reshape(r, nw * 64)[:, :n]
+    piv = np.array(pivots, dtype=np.int64)
+    free = np.setdiff1d(np.arange(n), piv)
+    kk = len(free) if k is None else int(k)
+    if kk > len(free):
+        raise ValueError("k = %d exceeds the code dimension %d" % (kk, len(free)))
+    info = free[:kk]
+    G = np.zeros((kk, n), dtype=np.uint8)
+    G[np.arange(kk), info] = 1
+    G[:, piv] = R[:, info].T
+    return G, info
+
+
 class LDPCEncoder:
     def __init__(self, n: int, k: int, H: Optional[np.ndarray] = None, G: Optional[np.ndarray] = None,
                  dv: int = 3, dc: int = 6, seed: Optional[int] = None):
@@ -106,6 +160,34 @@ class LDPCEncoder:
         syn = (msg @ (np.asarray(self.H[:, :self.k]).T)) % 2
         parity = _solve_gf2_batch(np.asarray(self.H[:, self.k:]), syn.T.astype(np.uint8)).T
         return np.hstack([msg, parity]).astype(int)
+
+    # ---- valid codewords on the device (SURVEY §8 f row 3) -------------------
+    def valid_generator(self):
+        """(G [k, n], info positions [k]) of valid_generator(H, k), cached."""
+        if getattr(self, "_valid", None) is None:
+            self._valid = valid_generator(self.H, self.k)
+        return self._valid
+
+    @property
+    def info_positions(self) -> np.ndarray:
+        return self.valid_generator()[1]
+
+    def encode_batch_device(self, messages, out=None):
+        """Valid codewords for a batch of k-bit messages on the device
+        (pl_gf2_encode): codeword[:, info_positions] = message.  messages: uint8
+        [B, k] CUDA tensor or array; returns a uint8 [B, n] CUDA tensor."""
+        import torch
+        from .. import _native
+        if getattr(self, "_g_dev", None) is None:
+            G, _ = self.valid_generator()
+            self._g_dev = torch.from_numpy(_native.pack_gf2_columns(G)).cuda()
+        msg = messages if isinstance(messages, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(np.asarray(messages), dtype=np.uint8))
+        msg = msg.to(device="cuda", dtype=torch.uint8).contiguous()
+        assert msg.dim() == 2 and msg.shape[1] == self.k, "messages must be [B, k]"
+        cw = out if out is not None else torch.empty((msg.shape[0], self.n), dtype=torch.uint8, device="cuda")
+        _native.gf2_encode(self._g_dev, self.k, self.n, msg, cw)
+        return cw
 
     def verify_codeword(self, codeword: np.ndarray) -> bool:
         return bool(np.all((self.H @ codeword) % 2 == 0))

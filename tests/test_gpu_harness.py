@@ -73,3 +73,44 @@ def test_cascl_ber_beats_scl(gpu):
     _, f_scl, _ = simulate_polar([-0.5], 8192, 10 ** 9, cfg, list_size=32, crc_polynomial=None, batch=8192)
     _, f_ca, p = simulate_polar([-0.5], 8192, 10 ** 9, cfg, list_size=32, crc_polynomial="CRC-8", batch=8192)
     assert p[0].frames == 8192 and f_scl[0] > 0.0 and f_ca[0] < f_scl[0]
+
+
+def test_ldpc_device_encoder_valid_codewords(gpu):
+    """pl_gf2_encode: device codewords equal msg . G (mod 2) on the host, satisfy
+    H, carry the message at info_positions, and decode back at high SNR."""
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.ldpc import BPDecoder, LDPCEncoder
+    enc = LDPCEncoder(504, 252, dv=3, dc=6, seed=42)
+    B = 4096
+    msg = torch.empty((B, 252), dtype=torch.uint8, device="cuda")
+    _native.random_bits(7, 0, msg)
+    cw = enc.encode_batch_device(msg)
+    G, info = enc.valid_generator()
+    m = msg.cpu().numpy().astype(np.int64)
+    c = cw.cpu().numpy().astype(np.int64)
+    assert np.array_equal(c, (m @ G.astype(np.int64)) % 2)
+    assert not ((np.asarray(enc.H).astype(np.int64) @ c.T) % 2).any()
+    assert np.array_equal(c[:, info], m)
+    llr = AWGNChannel(5.0).llr_batch_device(cw, 504, B, seed=3)
+    bits = BPDecoder(enc.H, 20).decode_batch(llr)  # device in, device out
+    assert np.array_equal(bits.cpu().numpy()[:, info], m)
+
+
+def test_ldpc_mc_random_codewords_match_zero_codeword(gpu):
+    """BP is codeword-symmetric: the FER with random valid codewords (device
+    encoder) agrees with the all-zero-codeword FER within Monte-Carlo error."""
+    from polarcode_and_ldpc_amd.harness.montecarlo import MonteCarlo, ldpc_round_fn, wilson_interval
+    from polarcode_and_ldpc_amd.ldpc import BPDecoder, LDPCEncoder
+    enc = LDPCEncoder(504, 252, dv=3, dc=6, seed=42)
+    dec = BPDecoder(enc.H, 20)
+    res = {}
+    for tag, e in (("zero", None), ("random", enc)):
+        mc = MonteCarlo(ldpc_round_fn(dec, seed=11, info_bits=252, encoder=e), info_bits=252, batch=32768)
+        p = mc.run([-1.0], 65536, 10 ** 9)[0]
+        res[tag] = p
+    fz, fr = res["zero"].fer, res["random"].fer
+    assert 0.005 < fz < 0.9
+    _, lo_z, hi_z = wilson_interval(res["zero"].frame_errors, res["zero"].frames, 0.999)
+    _, lo_r, hi_r = wilson_interval(res["random"].frame_errors, res["random"].frames, 0.999)
+    assert lo_z <= hi_r and lo_r <= hi_z, (fz, fr)

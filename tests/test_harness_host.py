@@ -99,3 +99,25 @@ def test_host_channels_follow_reference_rng_use():
     sd = np.sqrt(1.0 / (2.0 * 10 ** 0.1))
     y = h * s + np.random.normal(0, sd, 64)
     assert np.allclose(llr, 2.0 * y * h / sd ** 2, rtol=0, atol=0)
+
+
+def test_valid_generator_spans_the_code():
+    """§8 f row 3: the seed-42 (504, 252) H is rank-deficient (rank 251, rank of
+    H2 236), so the reference's encoders emit non-codewords; valid_generator's
+    rows are codewords, independent, with the message at `info`."""
+    from polarcode_and_ldpc_amd.ldpc import LDPCEncoder, regular_construction, valid_generator
+    from polarcode_and_ldpc_amd._native import pack_gf2_columns
+    enc = LDPCEncoder(504, 252, dv=3, dc=6, seed=42)
+    H = np.asarray(enc.H).astype(np.int64)
+    G, info = enc.valid_generator()
+    assert G.shape == (252, 504) and len(np.unique(info)) == 252
+    assert not ((H @ G.T.astype(np.int64)) % 2).any()
+    assert np.array_equal(G[:, info], np.eye(252, dtype=np.uint8))
+    assert not ((H @ np.asarray(enc.encode(np.ones(252, int))).astype(np.int64)) % 2 == 0).all()  # reference quirk
+    H2 = np.asarray(regular_construction(504, 3, 6, seed=3)).astype(np.int64)
+    G2, info2 = valid_generator(H2)
+    assert not ((H2 @ G2.T.astype(np.int64)) % 2).any() and G2.shape[0] == len(info2)
+    P = pack_gf2_columns(G).view(np.uint32)
+    i, j = 37, 411
+    assert ((P[i // 32, j] >> (i % 32)) & 1) == G[i, j]
+    assert P.shape == (8, 504)

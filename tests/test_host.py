@@ -14,7 +14,7 @@ from conftest import ROOT, golden
 def _header_symbols():
     txt = open(os.path.join(ROOT, "include", "polarldpc.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(pl_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(pl_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_library_exports_every_header_symbol():

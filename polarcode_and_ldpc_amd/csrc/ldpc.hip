@@ -194,9 +194,14 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
                 // np.prod over the masked messages, left to right (see ldpc_reg_kernel)
                 const double* lo = T + e0;
                 const double* hi = lo + 1;
+                const int nf = d - 1;
                 double p = 1.0;
-#pragma unroll 4
-                for (int k = 0; k < d - 1; ++k) p *= (k < i ? lo : hi)[k];
+                int k = 0;
+                for (; k + 4 <= nf; k += 4, lo += 4, hi += 4) {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) p *= (k + c < i ? lo : hi)[c];
+                }
+                for (; k < nf; ++k, ++lo, ++hi) p *= (k < i ? lo : hi)[0];
                 const bool pn = __builtin_isnan(p);
                 p = __builtin_fmax(__builtin_fmin(p, 0.999999), -0.999999);
                 o = OCML ? 2.0 * atanh(p) : two_atanh(p);
@@ -300,11 +305,24 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
             if (ALGO == 0) {
                 // np.prod over the masked messages, left to right: factor k of
                 // d-1 is T[e0 + k] before the own edge, T[e0 + k + 1] after it
+                // (two running LDS pointers, one select per factor; a guarded
+                // tail instead of a remainder loop)
                 const double* lo = T + e0;
                 const double* hi = lo + 1;
+                const int nf = d - 1;
                 double p = 1.0;
-#pragma unroll 4
-                for (int k = 0; k < d - 1; ++k) p *= (k < i ? lo : hi)[k];
+                int k = 0;
+                for (; k + 4 <= nf; k += 4, lo += 4, hi += 4) {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) p *= (k + c < i ? lo : hi)[c];
+                }
+                if (k < nf) {
+                    p *= (k < i ? lo : hi)[0];
+                    if (k + 1 < nf) {
+                        p *= (k + 1 < i ? lo : hi)[1];
+                        if (k + 2 < nf) p *= (k + 2 < i ? lo : hi)[2];
+                    }
+                }
                 // clip, 2*atanh, nan_to_num: after the clip 2*atanh is finite,
                 // so only a NaN product (NaN channel LLRs) maps to 0
                 const bool pn = __builtin_isnan(p);

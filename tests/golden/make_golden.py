@@ -379,8 +379,54 @@ def job_ldpc_special():
     return "ldpc_special.npz", out
 
 
+def job_polar_erasures():
+    """Erasures (LLR = 0), saturated LLRs, signed zeros and denormals through the
+    reference SC and SCL decoders: BEC-like frames (noiseless codewords as +-40
+    with 25-50 % erasures), AWGN frames with 20 % erasures, and mixed special
+    values (+-inf, +-0, +-1e-300, 1e300 on 1/8 of the positions).  BEC frames
+    with +-inf are kept for SC only: there the reference's g forms inf - inf =
+    NaN (decoder.py:417), and in SCL NaN path metrics make its list.sort order
+    an artefact of CPython's sort algorithm."""
+    polar, _, _ = _imp()
+    out = {}
+    for N, K, L in ((256, 128, 4), (1024, 512, 8)):
+        fr = bitrev_bhatta_frozen(N, K)
+        llr, msg, _ = _polar_frames(N, K, fr, (2.0,), 16, 77 + N)
+        rng = np.random.RandomState(N)
+        inf_llr = []
+        for f in range(len(llr)):
+            kind = f % 4
+            sgn = np.where(llr[f] >= 0, 1.0, -1.0)
+            if kind == 0:    # BEC, saturated finite
+                x = sgn * 40.0
+                x[rng.rand(N) < 0.25 + 0.25 * rng.rand()] = 0.0
+                llr[f] = x
+            elif kind == 1:  # AWGN with 20 % erasures
+                llr[f][rng.rand(N) < 0.2] = 0.0
+            elif kind == 2:  # mixed specials
+                idx = rng.choice(N, size=N // 8, replace=False)
+                llr[f][idx] = rng.choice([np.inf, -np.inf, 0.0, -0.0, 1e-300, -1e-300, 1e300], size=len(idx))
+            else:            # BEC with +-inf (SC only)
+                x = sgn * np.inf
+                x[rng.rand(N) < 0.25 + 0.25 * rng.rand()] = 0.0
+                inf_llr.append(x)
+                llr[f] = sgn * 40.0
+        sc = polar.SCDecoder(N, K, frozen_bits=fr)
+        scl = polar.SCLDecoder(N, K, list_size=L, frozen_bits=fr)
+        inf_llr = np.array(inf_llr)
+        out["N%d_frozen" % N] = fr
+        out["N%d_llr" % N] = llr
+        out["N%d_msg" % N] = msg
+        out["N%d_L" % N] = L
+        out["N%d_sc" % N] = np.array([sc.decode(l.copy()) for l in llr])
+        out["N%d_scl" % N] = np.array([scl.decode(l.copy()) for l in llr])
+        out["N%d_inf_llr" % N] = inf_llr
+        out["N%d_inf_sc" % N] = np.array([sc.decode(l.copy()) for l in inf_llr])
+    return "polar_erasures.npz", out
+
+
 JOBS = [job_scl4096_l8, job_scl1024_l8, job_ms8192, job_scl1024_l32, job_bp504,
-        job_sc1024, job_ms504, job_small, job_p1, job_kat16, job_crc, job_ldpc_special]
+        job_sc1024, job_ms504, job_small, job_p1, job_kat16, job_crc, job_ldpc_special, job_polar_erasures]
 
 
 def _run(fn):

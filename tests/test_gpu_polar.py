@@ -276,3 +276,28 @@ def test_cascl_decoder_class(gpu):
     mask[fr] = 1
     with pytest.raises(AssertionError):
         _native.polar_plan(N, K, mask, 0).set_crc(8, 0x1D)
+
+
+@pytest.mark.parametrize("flags", [0, 0x20, 0x10])
+def test_erasures_and_saturation_golden(gpu, flags):
+    """Erasures (LLR = 0), saturated LLRs, +-inf, signed zeros and denormals
+    against the reference's own outputs (golden polar_erasures.npz), SC and
+    SCL, on the tree (flags 0, where an instance exists), lane (0x20) and group
+    (0x10) kernels.  BEC frames with +-inf: SC only (see make_golden)."""
+    from polarcode_and_ldpc_amd import _native
+    d = golden("polar_erasures.npz")
+    for N in (256, 1024):
+        fr, L = d["N%d_frozen" % N], int(d["N%d_L" % N])
+        llr = torch.from_numpy(d["N%d_llr" % N]).cuda()
+        mask = np.zeros(N, np.uint8)
+        mask[fr] = 1
+        for lsz, key in ((0, "sc"), (L, "scl")):
+            plan = _native.polar_plan(N, N // 2, mask, lsz, flags=flags)
+            out = torch.empty((llr.shape[0], N // 2), dtype=torch.uint8, device="cuda")
+            plan.decode(llr, out)
+            assert _mismatch(out.cpu().numpy(), d["N%d_%s" % (N, key)]) == 0, (N, key, plan.info.reserved)
+        plan = _native.polar_plan(N, N // 2, mask, 0, flags=flags)  # +-inf BEC frames: SC only
+        inf = torch.from_numpy(d["N%d_inf_llr" % N]).cuda()
+        out = torch.empty((inf.shape[0], N // 2), dtype=torch.uint8, device="cuda")
+        plan.decode(inf, out)
+        assert _mismatch(out.cpu().numpy(), d["N%d_inf_sc" % N]) == 0, (N, "inf_sc", plan.info.reserved)

@@ -98,6 +98,16 @@ def test_ldpc_special_values(oracle):
     assert np.array_equal(b, d["ms_bits"])
 
 
+def test_polar_erasures_and_saturation(oracle):
+    """LLR = 0 erasures, +-inf, signed zeros, denormals (make_golden.job_polar_erasures)."""
+    d = golden("polar_erasures.npz")
+    for N in (256, 1024):
+        fr, llr, L = d["N%d_frozen" % N], d["N%d_llr" % N], int(d["N%d_L" % N])
+        assert _bad(oracle.sc_decode(N, fr, llr), d["N%d_sc" % N]) == 0
+        assert _bad(oracle.scl_decode(N, L, fr, llr, threads=4), d["N%d_scl" % N]) == 0
+        assert _bad(oracle.sc_decode(N, fr, d["N%d_inf_llr" % N]), d["N%d_inf_sc" % N]) == 0
+
+
 def test_ms_degree1_raises(oracle):
     d = golden("ldpc_bp_504.npz")
     with pytest.raises(ValueError):

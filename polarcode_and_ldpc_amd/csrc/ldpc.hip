@@ -251,8 +251,13 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
     double* C = T + E;
     uint32_t* syn = reinterpret_cast<uint32_t*>(smem + (size_t)16 * E);  // [2][m]
     uint8_t* bt = reinterpret_cast<uint8_t*>(syn + 2 * m);               // [n]
+    // BP: edges whose v2c needs a tanh (|x| <= 14.52 or NaN), compacted: [E]
+    // indices + a counter (ldpc_reg_lds_bytes)
+    int32_t* work = reinterpret_cast<int32_t*>(smem + (((size_t)16 * E + (size_t)8 * m + n + 15) & ~(size_t)15));
+    int32_t* wcnt = work + E;
     const double* __restrict__ ch = llr + frame * ld;
     auto tin = [&](double x) -> double { return ALGO == 0 ? tanh_half_clip(x) : x; };
+    const int lane = __lane_id();
 
     int meta[EPT];
 #pragma unroll
@@ -274,6 +279,7 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         chv[j] = ok ? ch[v] : 0.0;
     }
     for (int c = tid; c < 2 * m; c += NT) syn[c] = 0u;
+    if (tid == 0) *wcnt = 0;
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
         if (tid + j * NT < n) {
@@ -338,17 +344,51 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         for (int j = 0; j < VPT; ++j) {
             const int v = tid + j * NT;
             if (v >= n) break;
+            double c2v[DV];
             double sum = 0.0;  // np.sum over DV < 8 messages: sequential
 #pragma unroll
-            for (int k = 0; k < DV; ++k) sum += C[ve[j][k]];
+            for (int k = 0; k < DV; ++k) {
+                c2v[k] = C[ve[j][k]];
+                sum += c2v[k];
+            }
             const double total = chv[j] + sum;
             const bool one = total <= 0.0;
             bt[v] = one ? 1 : 0;
 #pragma unroll
             for (int k = 0; k < DV; ++k) {
-                T[ve[j][k]] = tin(total - C[ve[j][k]]);
+                const double x = total - c2v[k];  // v2c as decoder.py:120 forms it
+                if (ALGO == 0) {
+                    // saturated inputs take the clip value now; the rest are
+                    // appended to the work list and get their tanh below, in a
+                    // dense pass over all of the frame's threads
+                    const bool sat = fabs(x) > 14.52;
+                    T[ve[j][k]] = sat ? __builtin_copysign(0.999999, x) : x;
+                    const uint64_t need = __ballot(!sat);
+                    if (need) {
+                        const uint64_t act = __ballot(1);
+                        const int leader = __ffsll((unsigned long long)act) - 1;
+                        int base = 0;
+                        if (lane == leader) base = atomicAdd(wcnt, (int)__popcll(need));
+                        base = __builtin_amdgcn_readlane(base, leader);
+                        const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                        if (!sat) work[base + pre] = ve[j][k];
+                    }
+                } else {
+                    T[ve[j][k]] = x;
+                }
                 if (one) atomicXor(&scur[vc[j][k]], 1u);
             }
+        }
+        if (ALGO == 0) {
+            __syncthreads();
+            const int nw = *wcnt;
+            for (int w = tid; w < nw; w += NT) {
+                const int e = work[w];
+                T[e] = tanh_half_clip(T[e]);
+            }
+            __syncthreads();
+            if (tid == 0) *wcnt = 0;  // read by every thread before the barrier above
         }
         __syncthreads();
     }

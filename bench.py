@@ -86,6 +86,27 @@ def load_traffic(name):
         return None
 
 
+def load_valu(name):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        return float(json.load(open(p))[name]["valu_instr_per_launch"])
+    except Exception:
+        return None
+
+
+def _valu_rate(roof, name, cus, clock_ghz=2.4):
+    """VALU issue against its ceiling: SQ_INSTS_VALU (PMC, per launch) over the
+    live kernel time.  A CU issues at most one wave64 fp64 VALU instruction per
+    cycle (4 SIMDs, 4 cycles each), so peak = CUs x clock."""
+    v = load_valu(name)
+    if v is None:
+        return
+    rate = v / (roof["kernel_ms"] / 1e3) / 1e9  # G wave-instructions / s
+    peak = cus * clock_ghz
+    roof["valu"] = dict(instr_per_launch=v, achieved=rate, peak=peak, unit="G wave-instr/s (fp64 VALU)",
+                        frac=rate / peak, source="profiles/pmc_traffic.json (SQ_INSTS_VALU)")
+
+
 def traffic_source(name):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -155,6 +176,7 @@ def bench_polar(args, rank, world):
                              kernel_ms=kms),
                plan=dict(lds_bytes=plan.info.lds_bytes, fused_top=plan.info.fused_top))
     _traffic_rate(res["roofline"])
+    _valu_rate(res["roofline"], "polar_scl_1024_l8", torch.cuda.get_device_properties(0).multi_processor_count)
     c = counts.cpu().numpy()
     res["ber"] = float(c[0]) / max(1, c[2] * K)
     res["fer"] = float(c[1]) / max(1, c[2])
@@ -219,6 +241,8 @@ def bench_ldpc(args, rank, world):
                              kernel={2: "ldpc_reg_kernel<BP,DV=3>", 1: "ldpc_decode_kernel<BP>",
                                      3: "ldpc_check_kernel<BP>"}.get(plan.info.reserved, "?")))
     _traffic_rate(res["roofline"])
+    _valu_rate(res["roofline"], "ldpc_bp_504", torch.cuda.get_device_properties(0).multi_processor_count)
+    res["roofline"]["limit"] = "VALU issue (fp64 transcendentals), see roofline.valu; HBM fields are the algorithmic view"
     if rank == 0 and world == 1 and not args.skip_cpu:
         from oracle import oracle as O
         from polarcode_and_ldpc_amd.ldpc import dense_to_csr

@@ -22,3 +22,6 @@ echo "fetch ok $(date)" >> "$OUT/progress.txt"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
     python3 "$R/bench.py" --skip-cpu > /dev/null 2> "$OUT/pmc_write.err" || exit $?
 echo "write ok $(date)" >> "$OUT/progress.txt"
+timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d "$OUT/pmc_valu" -o run -- \
+    python3 "$R/bench.py" --skip-cpu > /dev/null 2> "$OUT/pmc_valu.err" || exit $?
+echo "valu ok $(date)" >> "$OUT/progress.txt"

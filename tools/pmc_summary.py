@@ -6,6 +6,8 @@ Writes <dst>/kernel_stats.csv (rocprofv3 --kernel-trace --stats summary),
 <dst>/pmc_summary.json (per-kernel mean FETCH_SIZE / WRITE_SIZE per launch) and
 updates profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
 
+SQ_INSTS_VALU (wave-level VALU instructions) per launch is recorded too when the
+pmc_valu pass exists.
 HBM traffic per launch = 2 * FETCH_SIZE + WRITE_SIZE (rocprofv3 reports KiB;
 FETCH_SIZE counts 64 B per 128 B request on gfx950 -> doubled, as
 MI355X_MICROARCH.md "HBM" prescribes; WRITE_SIZE is taken as reported).
@@ -38,11 +40,16 @@ def main(src, dst):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f))
     fetch = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
+    vp = os.path.join(src, "pmc_valu", "run_counter_collection.csv")
+    valu = per_kernel(vp) if os.path.exists(vp) else {}
     summ = {}
     for (name, _), v in fetch.items():
         w = write.get((name, "WRITE_SIZE"), 0.0)
         summ[name] = dict(fetch_size_kib=v, write_size_kib=w,
                           hbm_bytes_per_launch=2 * v * 1024 + w * 1024)
+        if (name, "SQ_INSTS_VALU") in valu:
+            summ[name]["valu_instr_per_launch"] = valu[(name, "SQ_INSTS_VALU")]
+            summ[name]["waves_per_launch"] = valu.get((name, "SQ_WAVES"))
     json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
     tp = os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_traffic.json")
     traffic = json.load(open(tp)) if os.path.exists(tp) else {}
@@ -51,6 +58,8 @@ def main(src, dst):
             if name.startswith(prefix):
                 traffic[key] = dict(bytes_per_launch=s["hbm_bytes_per_launch"], source=os.path.join(dst, "pmc_summary.json"),
                                     kernel=name.split("(")[0])
+                if "valu_instr_per_launch" in s:
+                    traffic[key]["valu_instr_per_launch"] = s["valu_instr_per_launch"]
     json.dump(traffic, open(tp, "w"), indent=1)
     for name, s in summ.items():
         if s["hbm_bytes_per_launch"] > 1e6:

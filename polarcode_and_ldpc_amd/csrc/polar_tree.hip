@@ -429,27 +429,71 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 lds_sync();
                 // rank of (slot, b) in the stable descending order of
                 // [(m0, q) for active q] + [(m1, q) for active q]
-                int r0 = 0, r1 = 0;
                 constexpr int QC = LCAP < 8 ? LCAP : 8;
-                for (int q0 = 0; q0 < nact; q0 += QC) {
-                    double2 mq[QC];
+                auto exact_ranks = [&](int& r0, int& r1) {
+                    r0 = 0;
+                    r1 = 0;
+                    for (int q0 = 0; q0 < nact; q0 += QC) {
+                        double2 mq[QC];
 #pragma unroll
-                    for (int k = 0; k < QC; ++k) mq[k] = met[q0 + k];
+                        for (int k = 0; k < QC; ++k) mq[k] = met[q0 + k];
 #pragma unroll
-                    for (int k = 0; k < QC; ++k) {
-                        const int q = q0 + k;
-                        const bool v = q < nact;
-                        const double a = mq[k].x, b = mq[k].y;
-                        r0 += v & ((a > m0) | ((a == m0) & (q < slot)));
-                        r0 += v & (b > m0);
-                        r1 += v & (a >= m1);
-                        r1 += v & ((b > m1) | ((b == m1) & (q < slot)));
+                        for (int k = 0; k < QC; ++k) {
+                            const int q = q0 + k;
+                            const bool v = q < nact;
+                            const double a = mq[k].x, b = mq[k].y;
+                            r0 += v & ((a > m0) | ((a == m0) & (q < slot)));
+                            r0 += v & (b > m0);
+                            r1 += v & (a >= m1);
+                            r1 += v & ((b > m1) | ((b == m1) & (q < slot)));
+                        }
                     }
-                }
+                };
                 const int nsurv = (2 * nact < Lsz) ? 2 * nact : Lsz;
-                if (slot < nact) {
-                    if (r0 < nsurv) surv[r0] = (uint32_t)(slot << 1);
-                    if (r1 < nsurv) surv[r1] = (uint32_t)((slot << 1) | 1);
+                const uint32_t id0 = (uint32_t)(slot << 1), id1 = id0 | 1u;
+                int r0, r1;
+                if constexpr (LCAP >= 16 || NL >= 11) {
+                    // Large lists / long codes: strict comparisons only -- exact unless two
+                    // candidates tie (inactive slots publish -inf and never
+                    // count).  A tie makes two candidates claim one survivor
+                    // slot; the loser sees it and the wave redoes the ranks with
+                    // the stable tie-break.  (L = 32: 9.1 -> 7.5 ms, L = 16:
+                    // 7.7 -> 7.0 ms, N = 2048 / 4096 L = 8: ~2 %; at N = 1024,
+                    // L <= 8 the check costs more than it saves.)
+                    r0 = 0;
+                    r1 = 0;
+                    for (int q0 = 0; q0 < nact; q0 += QC) {
+                        double2 mq[QC];
+#pragma unroll
+                        for (int k = 0; k < QC; ++k) mq[k] = met[q0 + k];
+#pragma unroll
+                        for (int k = 0; k < QC; ++k) {
+                            const double a = mq[k].x, b = mq[k].y;
+                            r0 += (a > m0) + (b > m0);
+                            r1 += (a > m1) + (b > m1);
+                        }
+                    }
+                    if (slot < nact) {
+                        if (r0 < nsurv) surv[r0] = id0;
+                        if (r1 < nsurv) surv[r1] = id1;
+                    }
+                    lds_sync();
+                    const bool lost =
+                        slot < nact && ((r0 < nsurv && surv[r0] != id0) || (r1 < nsurv && surv[r1] != id1));
+                    if (__ballot(lost)) {
+                        exact_ranks(r0, r1);
+                        lds_sync();  // every lane has read surv before it is rewritten
+                        if (slot < nact) {
+                            if (r0 < nsurv) surv[r0] = id0;
+                            if (r1 < nsurv) surv[r1] = id1;
+                        }
+                    }
+                } else {
+                    exact_ranks(r0, r1);
+                    if (slot < nact) {
+                        if (r0 < nsurv) surv[r0] = id0;
+                        if (r1 < nsurv) surv[r1] = id1;
+                    }
                 }
                 lds_sync();
                 bit = 0;

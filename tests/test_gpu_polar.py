@@ -301,3 +301,21 @@ def test_erasures_and_saturation_golden(gpu, flags):
         out = torch.empty((inf.shape[0], N // 2), dtype=torch.uint8, device="cuda")
         plan.decode(inf, out)
         assert _mismatch(out.cpu().numpy(), d["N%d_inf_sc" % N]) == 0, (N, "inf_sc", plan.info.reserved)
+
+
+@pytest.mark.parametrize("L", [16, 32])
+def test_large_list_ties_vs_oracle(gpu, oracle, L):
+    """Erasure-heavy frames make path metrics tie (LLR = 0 gives m0 = m1), which
+    sends the large-list kernels' strict-comparison ranking to its stable
+    tie-break fallback: every frame must still match the oracle."""
+    from polarcode_and_ldpc_amd import _native
+    d = golden("polar_erasures.npz")
+    fr, llr = d["N1024_frozen"], d["N1024_llr"]
+    mask = np.zeros(1024, np.uint8)
+    mask[fr] = 1
+    want = oracle.scl_decode(1024, L, fr, llr, threads=8)
+    plan = _native.polar_plan(1024, 512, mask, L)
+    assert plan.info.reserved == 4
+    out = torch.empty((llr.shape[0], 512), dtype=torch.uint8, device="cuda")
+    plan.decode(torch.from_numpy(llr).cuda(), out)
+    assert _mismatch(out.cpu().numpy(), want) == 0

@@ -193,6 +193,12 @@ def bench_polar(args, rank, world):
                                    sample="first %d frames of the same LLR batch, oracle/refcpu.c SCL L=%d "
                                           "(loop-faithful C restatement, OpenMP %d threads), %.1f s" % (S, L, th, ct),
                                    mismatching_frames_vs_gpu=int((ref != got).any(axis=1).sum()))
+        S1 = max(1, S // 16)  # single-core figure, same frames
+        t0 = time.perf_counter()
+        O.scl_decode(N, L, frozen, llr_h[:S1], threads=1)
+        c1 = time.perf_counter() - t0
+        res["cpu_baseline"]["single_core"] = dict(value=S1 * K / c1 / 1e6, unit="info-Mbps", cores=1,
+                                                  sample="first %d frames, 1 thread, %.1f s" % (S1, c1))
     return res
 
 
@@ -258,6 +264,12 @@ def bench_ldpc(args, rank, world):
                                    sample="first %d frames of the same batch, oracle/refcpu.c BP-20, %d threads, "
                                           "%.1f s" % (S, th, ct),
                                    mismatching_frames_vs_gpu=int((rb != got).any(axis=1).sum()))
+        S1 = max(1, S // 16)
+        t0 = time.perf_counter()
+        O.ldpc_decode(rp, ci, n, llr_h[:S1], "bp", 20, True, 1.0, threads=1)
+        c1 = time.perf_counter() - t0
+        res["cpu_baseline"]["single_core"] = dict(value=S1 * k / c1 / 1e6, unit="info-Mbps", cores=1,
+                                                  sample="first %d frames, 1 thread, %.1f s" % (S1, c1))
     return res
 
 

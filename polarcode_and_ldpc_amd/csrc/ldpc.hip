@@ -12,12 +12,17 @@
 // np.sum over the incoming messages is NumPy's pairwise_sum (sequential below 8
 // terms, 8 accumulators up to 128); reproduced exactly.
 //
-// Mapping (DESIGN.md §LDPC kernel): one workgroup decodes one frame; messages
-// are stored as c2v[E] plus total[n] (v2c = total - c2v, exactly how the
-// reference forms it), so the check phase, the leave-one-out phase and the
-// variable phase are each one pass over edges / variables in LDS (or in the
-// global workspace for codes whose state does not fit LDS).  Edges are laid out
-// check-major (CSR of H) so a check's inputs are contiguous.
+// Mapping (DESIGN.md §4 LDPC kernels): one workgroup decodes one frame.  State
+// T[E] (check inputs) + C[E] (check-to-variable) in LDS, v2c = total - c2v
+// exactly as the reference forms it; edges check-major (CSR of H, checks
+// degree-sorted) so a check's inputs are contiguous.  Kernels:
+//   ldpc_reg_kernel<ALGO, DV, EPT, VPT>  constant variable degree: adjacency and
+//                                        channel LLRs in registers, BP tanh via a
+//                                        compacted work list (the BASELINE codes);
+//   ldpc_decode_kernel<ALGO, GLOBAL, ..> any code, LDS or global-workspace state;
+//   ldpc_ms_compact_kernel               min-sum for codes whose T/C exceed LDS:
+//                                        compressed per-check statistics in LDS;
+//   ldpc_check_kernel<ALGO>              thread-per-check variant (diagnostic).
 #include "common.hpp"
 #include "internal.hpp"
 #include "fp64_math.hpp"

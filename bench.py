@@ -6,7 +6,10 @@ Headline (`value`): Polar N=1024 K=512 SCL L=8, 65 536 AWGN frames per GPU
 matrix + on-device error count (+ one all-reduce of the counters when N > 1).
 Secondary (`ldpc`): LDPC (504,252) BP max_iter=20 (configs[2]) on the
 reference harness's frames (benchmarks/throughput_test.py:285-315: its encoder's
-invalid codewords, so every frame runs all 20 iterations).
+invalid codewords, so every frame runs all 20 iterations); `ldpc.valid_codewords`
+is the same decode on valid (all-zero) codewords with early stop.
+`end_to_end`: the polar Monte-Carlo step with fresh device messages, encoding and
+AWGN inside the timed region (SURVEY §8 d "end-to-end MC").
 
 info-Mbps = frames * K_info / t / 1e6 (throughput_test.py:217, :304).
 Usage: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torchrun.
@@ -148,11 +151,15 @@ def bench_polar(args, rank, world):
     counts = torch.zeros(3, dtype=torch.int64, device="cuda")
     kt = KernelTimer()
 
+    sc = torch.zeros(3, dtype=torch.int64, device="cuda")  # this step's counters
+
     def step():
         kt(lambda: plan.decode(llr, out))
-        _native.count_errors(msg, out, K, counts)
+        sc.zero_()
+        _native.count_errors(msg, out, K, sc)
         if world > 1:
-            dist.all_reduce(counts)
+            dist.all_reduce(sc)
+        counts.add_(sc)
 
     dt = timed_steps(step, args.steps, args.warmup, world)
     kms = kt.mean_ms()  # includes warmup launches; steady state
@@ -180,6 +187,35 @@ def bench_polar(args, rank, world):
     c = counts.cpu().numpy()
     res["ber"] = float(c[0]) / max(1, c[2] * K)
     res["fer"] = float(c[1]) / max(1, c[2])
+
+    # End-to-end Monte Carlo (SURVEY §8 d): each step draws fresh messages,
+    # encodes, adds AWGN and decodes on the device, then counts errors.
+    ch = AWGNChannel(args.snr)
+    e2e_counts = torch.zeros(3, dtype=torch.int64, device="cuda")
+    e2e_step_no = [0]
+    msg2, cw2, out2 = torch.empty_like(msg), torch.empty_like(cw), torch.empty_like(out)
+    llr2 = torch.empty_like(llr)
+
+    def e2e_step():
+        o = off + e2e_step_no[0] * B * world  # fresh global frame indices every step
+        e2e_step_no[0] += 1
+        _native.random_bits(43, o, msg2)
+        _native.polar_encode(plan, msg2, cw2)
+        ch.llr_batch_device(cw2, N, B, seed=43, frame_offset=o, out=llr2)
+        plan.decode(llr2, out2)
+        sc.zero_()
+        _native.count_errors(msg2, out2, K, sc)
+        if world > 1:
+            dist.all_reduce(sc)
+        e2e_counts.add_(sc)
+
+    edt = timed_steps(e2e_step, args.steps, args.warmup, world)
+    ec = e2e_counts.cpu().numpy()
+    res["end_to_end"] = dict(value=B * world * args.steps * K / edt / 1e6, unit="info-Mbps",
+                             ms_per_step=edt / args.steps * 1e3,
+                             what="per step: device random messages + polar encode + AWGN LLRs (Philox) + "
+                                  "SCL decode + error count (+ all-reduce)",
+                             ber=float(ec[0]) / max(1, ec[2] * K), fer=float(ec[1]) / max(1, ec[2]))
     if rank == 0 and world == 1 and not args.skip_cpu:
         from oracle import oracle as O
         S = args.cpu_frames
@@ -220,11 +256,15 @@ def bench_ldpc(args, rank, world):
     counts = torch.zeros(3, dtype=torch.int64, device="cuda")
     kt = KernelTimer()
 
+    sc = torch.zeros(3, dtype=torch.int64, device="cuda")
+
     def step():
         kt(lambda: plan.decode(llr, out, its))
-        _native_count(cw, out, k, counts)
+        sc.zero_()
+        _native_count(cw, out, k, sc)
         if world > 1:
-            dist.all_reduce(counts)
+            dist.all_reduce(sc)
+        counts.add_(sc)
 
     from polarcode_and_ldpc_amd._native import count_errors as _native_count
     dt = timed_steps(step, args.steps, args.warmup, world)
@@ -249,6 +289,21 @@ def bench_ldpc(args, rank, world):
     _traffic_rate(res["roofline"])
     _valu_rate(res["roofline"], "ldpc_bp_504", torch.cuda.get_device_properties(0).multi_processor_count)
     res["roofline"]["limit"] = "VALU issue (fp64 transcendentals), see roofline.valu; HBM fields are the algorithmic view"
+    # Second frame source (SURVEY §8 d): valid codewords (all-zero; BP is
+    # codeword-symmetric) at the same SNR, early stop on.
+    llr0 = AWGNChannel(args.snr).llr_batch_device(None, n, B, seed=4243, frame_offset=rank * B)
+    out0 = torch.empty_like(out)
+    its0 = torch.empty_like(its)
+
+    def step0():
+        plan.decode(llr0, out0, its0)
+
+    dt0 = timed_steps(step0, args.steps, args.warmup, world)
+    res["valid_codewords"] = dict(value=B * world * args.steps * k / dt0 / 1e6, unit="info-Mbps",
+                                  ms_per_step=dt0 / args.steps * 1e3,
+                                  mean_iterations=float(its0.double().mean().item()),
+                                  bit_errors=int(out0.sum().item()),
+                                  what="all-zero codeword frames (device AWGN), BP max_iter=20, early stop")
     if rank == 0 and world == 1 and not args.skip_cpu:
         from oracle import oracle as O
         from polarcode_and_ldpc_amd.ldpc import dense_to_csr
@@ -309,6 +364,7 @@ def main():
             "roofline": pol["roofline"],
             "cpu_baseline": pol.get("cpu_baseline"),
             "ber": pol["ber"], "fer": pol["fer"], "plan": pol["plan"],
+            "end_to_end": pol["end_to_end"],
         }
         if ldp is not None:
             line["ldpc"] = ldp

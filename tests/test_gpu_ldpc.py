@@ -180,3 +180,16 @@ def test_special_values_golden(gpu, algo, kernel, monkeypatch):
     assert np.array_equal(got_b, d[algo + "_bits"])
     if algo == "bp":
         assert np.array_equal(got_i, d["bp_iters"])
+
+
+def test_empty_batch(gpu):
+    """A zero-frame batch returns empty bits and iteration counts (BP and MS)."""
+    d = golden("ldpc_bp_504.npz")
+    L = _L()
+    H = _H(d)
+    for dec in (L.BPDecoder(H, max_iter=20), L.MSDecoder(_H(golden("ldpc_ms_504.npz")), max_iter=20),
+                L.MSDecoder(_H(golden("ldpc_ms_8192.npz")), max_iter=20)):
+        bits = dec.decode_batch(np.zeros((0, dec.n)))
+        assert bits.shape == (0, dec.n)
+    bits, its = L.BPDecoder(H, max_iter=20).decode_batch(np.zeros((0, 504)), return_iterations=True)
+    assert bits.shape == (0, 504) and its.shape == (0,)

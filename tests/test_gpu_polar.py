@@ -319,3 +319,14 @@ def test_large_list_ties_vs_oracle(gpu, oracle, L):
     out = torch.empty((llr.shape[0], 512), dtype=torch.uint8, device="cuda")
     plan.decode(torch.from_numpy(llr).cuda(), out)
     assert _mismatch(out.cpu().numpy(), want) == 0
+
+
+def test_empty_batch(gpu):
+    """A zero-frame batch decodes to an empty [0, K] result (SC, SCL tree and
+    lane kernels) without launching."""
+    P = _P()
+    for dec in (P.SCDecoder(1024, 512), P.SCLDecoder(1024, 512, list_size=8), P.SCLDecoder(512, 256, list_size=4)):
+        got = dec.decode_batch(np.zeros((0, dec.N)))
+        assert got.shape == (0, dec.K)
+        got = dec.decode_batch(torch.zeros((0, dec.N), dtype=torch.float64, device="cuda"))
+        assert tuple(got.shape) == (0, dec.K)

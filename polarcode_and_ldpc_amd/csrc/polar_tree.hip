@@ -138,14 +138,14 @@ struct Fold {
 // (even, odd) pair to this lane's slot and continue one depth down with f.
 // Compile-time recursion keeps every pending value in a register.
 template <class G, int D>
-PL_DEV void fold(Fold<G>& st, double v, int idx, unsigned char* smem, unsigned char* ws, int lane) {
+PL_DEV void fold(Fold<G>& st, double v, int idx, unsigned char* smem, unsigned char* ws, int plane) {
     if constexpr (D == G::n) {
         st.lam = v;
     } else {
         if (idx & 1) {
             double2* dst = reinterpret_cast<double2*>((D >= G::DL ? smem : ws) + G::llr_off(D));
-            dst[(idx >> 1) * 64 + lane] = make_double2(st.pend[D], v);
-            fold<G, D + 1>(st, f_ms(st.pend[D], v), idx >> 1, smem, ws, lane);
+            dst[(idx >> 1) * 64 + plane] = make_double2(st.pend[D], v);
+            fold<G, D + 1>(st, f_ms(st.pend[D], v), idx >> 1, smem, ws, plane);
         } else {
             st.pend[D] = v;
         }
@@ -155,7 +155,7 @@ PL_DEV void fold(Fold<G>& st, double v, int idx, unsigned char* smem, unsigned c
 // Right child at depth Q = P+1: g over the parent pairs (slot ps) with the left
 // sibling's partial sums, then the f-chain down to the leaf.
 template <class G, int P>
-PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int lane, int ps, int bs, uint32_t bb,
+PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int plane, int ps, int bs, uint32_t bb,
                         uint32_t bw5) {
     constexpr int n = G::n, Q = P + 1, SQ = 1 << (n - Q);
     Fold<G> st;
@@ -175,7 +175,7 @@ PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int lane, int ps
         }
 #pragma unroll
         for (int k = 0; k < U; ++k)
-            fold<G, Q>(st, g_op(pr[k].x, pr[k].y, w >> ((t0 + k) & 31)), t0 + k, smem, ws, lane);
+            fold<G, Q>(st, g_op(pr[k].x, pr[k].y, w >> ((t0 + k) & 31)), t0 + k, smem, ws, plane);
     }
     return st.lam;
 }
@@ -185,7 +185,7 @@ PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int lane, int ps
 // children): depth-F elements from 2^(F-D0) values each (level d is g where the
 // depth-d ancestor of leaf i is a right child), then the f-chain to the leaf.
 template <class G, int D0>
-PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int fw, const double* ch,
+PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int fw, int plane, const double* ch,
                          const bool* right, const uint32_t* const* bsrc, uint32_t* bw) {
     constexpr int n = G::n, F = G::F, SF = 1 << (n - F), W = 1 << (F - D0);
     Fold<G> st;
@@ -240,7 +240,7 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
                         for (int k = 0; k < m; ++k) v[k] = f_ms(v[2 * k], v[2 * k + 1]);
                     }
                 }
-                fold<G, F>(st, v[0], t, smem, ws, lane);
+                fold<G, F>(st, v[0], t, smem, ws, plane);
             }
         }
         return st.lam;
@@ -274,14 +274,14 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
                 for (int k = 0; k < m; ++k) v[k] = f_ms(v[2 * k], v[2 * k + 1]);
             }
         }
-        fold<G, F>(st, v[0], t, smem, ws, lane);
+        fold<G, F>(st, v[0], t, smem, ws, plane);
     }
     return st.lam;
 }
 
 template <class G>
-PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, int fw, int i, const double* ch,
-                            uint64_t brow, int base, uint32_t bb, uint32_t bw5) {
+PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, int fw, int plane, int i,
+                            const double* ch, uint64_t brow, uint32_t bb, uint32_t bw5) {
     constexpr int n = G::n, F = G::F;
     bool right[F + 1];
     const uint32_t* bsrc[F + 1];
@@ -289,29 +289,30 @@ PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, in
 #pragma unroll
     for (int d = 1; d <= F; ++d) {
         right[d] = (i >> (n - d)) & 1;
-        bsrc[d] = reinterpret_cast<const uint32_t*>(ws + G::bl_off(d <= G::NB ? d : 1)) + base + field(brow, d);
+        bsrc[d] = reinterpret_cast<const uint32_t*>(ws + G::bl_off(d <= G::NB ? d : 1)) +
+                  field(brow, d) * G::FPW + fw;
         bw[d] = (d > G::NB) ? beta_get<n>(d, bb, bw5) : 0u;
     }
     if constexpr (G::NS >= 3) {
-        if (!right[1] && !right[2] && !right[3]) return fused_loop<G, 3>(smem, ws, lane, fw, ch, right, bsrc, bw);
+        if (!right[1] && !right[2] && !right[3]) return fused_loop<G, 3>(smem, ws, lane, fw, plane, ch, right, bsrc, bw);
     }
     if constexpr (G::NS >= 2) {
-        if (!right[1] && !right[2]) return fused_loop<G, 2>(smem, ws, lane, fw, ch, right, bsrc, bw);
+        if (!right[1] && !right[2]) return fused_loop<G, 2>(smem, ws, lane, fw, plane, ch, right, bsrc, bw);
     }
     if constexpr (G::NS >= 1) {
-        if (!right[1]) return fused_loop<G, 1>(smem, ws, lane, fw, ch, right, bsrc, bw);
+        if (!right[1]) return fused_loop<G, 1>(smem, ws, lane, fw, plane, ch, right, bsrc, bw);
     }
-    return fused_loop<G, 0>(smem, ws, lane, fw, ch, right, bsrc, bw);
+    return fused_loop<G, 0>(smem, ws, lane, fw, plane, ch, right, bsrc, bw);
 }
 
 template <class G, int P>
-PL_DEV double descend_from(int p, unsigned char* smem, unsigned char* ws, int lane, int ps, int bs, uint32_t bb,
+PL_DEV double descend_from(int p, unsigned char* smem, unsigned char* ws, int plane, int ps, int bs, uint32_t bb,
                            uint32_t bw5) {
     if constexpr (P >= G::n) {
         return 0.0;
     } else {
-        if (p == P) return descend_g<G, P>(smem, ws, lane, ps, bs, bb, bw5);
-        return descend_from<G, P + 1>(p, smem, ws, lane, ps, bs, bb, bw5);
+        if (p == P) return descend_g<G, P>(smem, ws, plane, ps, bs, bb, bw5);
+        return descend_from<G, P + 1>(p, smem, ws, plane, ps, bs, bb, bw5);
     }
 }
 
@@ -328,6 +329,13 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
     const int fw = lane / LCAP, slot = lane % LCAP, base = fw * LCAP;
+    // Workspace / LDS pools, partial sums and walk buffers are slot-major: path
+    // slot s of the wave's frame f lives in plane s * FPW + f, so the wave's
+    // slot-0 entries share one 128-byte line.  While the list is still growing
+    // (slot >= nact) a lane shadows slot 0: it takes slot 0's survivor entry at
+    // every pruning (same rows, partial sums and bit; metric -inf), uses slot
+    // 0's plane, and so loads the lines slot 0 loads and stores the values
+    // slot 0 stores to the same addresses -- no memory traffic of its own.
     unsigned char* const ws = workspace + (size_t)blockIdx.x * G::WS;
     uint64_t own = 0;
 #pragma unroll
@@ -336,7 +344,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
     uint64_t* const rowx = reinterpret_cast<uint64_t*>(smem + G::L_ROW + fw * G::GS);  // [LCAP][2]
     uint64_t* const brx = reinterpret_cast<uint64_t*>(smem + G::L_BR) + base;          // [LCAP]
     uint32_t* const surv = reinterpret_cast<uint32_t*>(smem + G::L_SURV) + base;       // [LCAP]
-    uint32_t* const walk = reinterpret_cast<uint32_t*>(ws + G::W_WALK) + lane;          // [2][CW][64]
+    uint32_t* const walk0 = reinterpret_cast<uint32_t*>(ws + G::W_WALK) + fw;           // [2][CW][64]
 
     unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tprev = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
@@ -380,7 +388,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 }
             }
         }
-        uint64_t lrow = own, brow = own;
+        uint64_t lrow = 0, brow = 0;  // slot 0's own rows; the other lanes shadow it
         uint32_t bb = 0, bw5 = 0;
         double pm = (slot == 0) ? 0.0 : -INFINITY;
         int nact = 1;
@@ -390,19 +398,21 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         for (int i = 0; i < N; ++i) {
             // ================================================ LLRs down to leaf i
             const int dstart = (i == 0) ? 1 : n - __builtin_ctz(i);
+            const int pslot = slot < nact ? slot : 0;  // shadows use slot 0's planes
+            const int plane = pslot * FPW + fw;
             double lam;
             if (dstart <= DL) ws_sync();  // workspace written by other lanes
             STAMP(7);
             if (dstart <= F) {
-                lam = descend_fused<G>(smem, ws, lane, fw, i, ch, brow, base, bb, bw5);
-                lrow = set_range(lrow, own, F, n);
+                lam = descend_fused<G>(smem, ws, lane, fw, plane, i, ch, brow, bb, bw5);
+                lrow = set_range(lrow, slot < nact ? own : 0ull, F, n);
                 STAMP(0);
             } else {
                 const int p = dstart - 1;
-                const int ps = base + field(lrow, p);
-                const int bs = base + field(brow, dstart <= G::NB ? dstart : 0);
-                lam = descend_from<G, F>(p, smem, ws, lane, ps, bs, bb, bw5);
-                lrow = set_range(lrow, own, dstart, n);
+                const int ps = field(lrow, p) * FPW + fw;
+                const int bs = field(brow, dstart <= G::NB ? dstart : 0) * FPW + fw;
+                lam = descend_from<G, F>(p, smem, ws, plane, ps, bs, bb, bw5);
+                lrow = set_range(lrow, slot < nact ? own : 0ull, dstart, n);
                 if (p < DL) { STAMP(1); } else { STAMP(2); }
             }
 
@@ -496,20 +506,19 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     }
                 }
                 lds_sync();
-                bit = 0;
-                if (slot < nsurv) {
-                    const uint32_t e = surv[slot];
+                {
+                    // survivor `slot` (decoder.py:323-336); lanes beyond the
+                    // survivors shadow survivor 0 (see `plane`) with metric -inf
+                    const uint32_t e = surv[slot < nsurv ? slot : 0];
                     const int par = (int)(e >> 1);
                     bit = (int)(e & 1u);
                     const double2 pmv = met[par];
-                    pm = bit ? pmv.y : pmv.x;
+                    pm = slot < nsurv ? (bit ? pmv.y : pmv.x) : -INFINITY;
                     lrow = rowx[2 * par];
                     brow = rowx[2 * par + 1];
                     const uint64_t br = brx[par];
                     bb = (uint32_t)br;
                     bw5 = (uint32_t)(br >> 32);
-                } else {
-                    pm = -INFINITY;
                 }
                 nact = nsurv;
                 lds_sync();  // scratch reads done before the next leaf's writes
@@ -532,29 +541,34 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 if (k == steps) {
                     beta_set<n>(dd, cur, bb, bw5);  // dd >= n-5: a left child, kept in registers
                 } else {
-                    // dd == n-5, cur = one word: multi-word combine through the workspace
+                    // dd == n-5, cur = one word: multi-word combine through the workspace.
+                    // Planes from the list size after this leaf's pruning: a lane that
+                    // just stopped shadowing slot 0 writes its own.
+                    const int wslot = slot < nact ? slot : 0;
+                    uint32_t* const walkw = walk0 + wslot * FPW;
                     int parity = 0;
                     ws_sync();  // multi-word betas of other lanes live in the workspace
-                    walk[0] = cur;
+                    walkw[0] = cur;
                     for (; k < steps; ++k) {
                         const int cwc = 1 << (k - 5);
-                        const int ls = base + field(brow, dd <= G::NB ? dd : 0);
+                        const int ls = field(brow, dd <= G::NB ? dd : 0) * FPW + fw;
                         const bool last = (k + 1 == steps);
                         const uint32_t* lsrc = reinterpret_cast<const uint32_t*>(ws + G::bl_off(dd <= G::NB ? dd : 1)) + ls;
-                        uint32_t* ldst = reinterpret_cast<uint32_t*>(ws + G::bl_off(dd - 1 >= 1 ? dd - 1 : 1)) + lane;
+                        uint32_t* ldst = reinterpret_cast<uint32_t*>(ws + G::bl_off(dd - 1 >= 1 ? dd - 1 : 1)) +
+                                         wslot * FPW + fw;
                         for (int w = 0; w < 2 * cwc; ++w) {
-                            const uint32_t cwv = walk[(parity * G::CW + (w >> 1)) * 64];
+                            const uint32_t cwv = walkw[(parity * G::CW + (w >> 1)) * 64];
                             const uint32_t lw = (dd > G::NB) ? bw5 : lsrc[(w >> 1) * 64];
                             const int sh = (w & 1) * 16;
                             const uint32_t r = spread16((lw ^ cwv) >> sh) | (spread16(cwv >> sh) << 1);
                             if (last && dd - 1 > 0) ldst[w * 64] = r;
-                            else walk[((parity ^ 1) * G::CW + w) * 64] = r;
+                            else walkw[((parity ^ 1) * G::CW + w) * 64] = r;
                         }
                         parity ^= 1;
                         --dd;
                     }
                     if (dd == 0) root_par = parity;
-                    else brow = set_field(brow, dd, slot);
+                    else brow = set_field(brow, dd, wslot);
                 }
             }
             lds_sync();
@@ -562,6 +576,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         }
 
         // ================================================ best path, output
+        uint32_t* const walk = walk0 + (slot < nact ? slot : 0) * FPW;
         int best = 0;
         if constexpr (!SC) {
             met[slot] = make_double2(pm, 0.0);

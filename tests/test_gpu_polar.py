@@ -330,3 +330,29 @@ def test_empty_batch(gpu):
         assert got.shape == (0, dec.K)
         got = dec.decode_batch(torch.zeros((0, dec.N), dtype=torch.float64, device="cuda"))
         assert tuple(got.shape) == (0, dec.K)
+
+
+@pytest.mark.parametrize("N,L", [(1024, 8), (1024, 32), (2048, 8), (4096, 8), (256, 16)])
+def test_list_growth_at_multiword_walks(gpu, oracle, N, L):
+    """The list grows (1 -> 2 -> 4 -> ...) at decode steps with many trailing
+    ones, where the partial-sum walk goes through the multi-word workspace
+    depths: lanes that stop shadowing slot 0 at such a step must write their
+    own planes.  Frozen set: all-frozen prefix, then info bits at steps
+    2^k - 1 first; noisy frames; tree kernel vs the C oracle, bit-exact."""
+    P = _P()
+    n = N.bit_length() - 1
+    K = N // 2
+    br = np.array([int(format(i, "0%db" % n)[::-1], 2) for i in range(N)])  # decode step -> u index
+    first = [s for s in (N // 16 - 1, N // 8 - 1, N // 4 - 1, 3 * N // 8 - 1, N // 2 - 1) if s > 0]
+    rest = [s for s in range(N - 1, -1, -1) if s not in first][:K - len(first)]
+    info_steps = sorted(set(first) | set(rest))
+    assert len(info_steps) == K
+    fr = np.setdiff1d(np.arange(N), br[info_steps])
+    rng = np.random.RandomState(N + L)
+    B = 16
+    snr = rng.uniform(0.0, 2.0, size=(B, 1))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+    llr = 2.0 * (1.0 + sigma * rng.randn(B, N)) / sigma ** 2
+    want = oracle.scl_decode(N, L, fr, llr, threads=8)
+    got = P.SCLDecoder(N, K, list_size=L, frozen_bits=fr).decode_batch(llr)
+    assert _mismatch(got, want) == 0

@@ -188,6 +188,8 @@ def bench_polar(args, rank, world):
     res["ber"] = float(c[0]) / max(1, c[2] * K)
     res["fer"] = float(c[1]) / max(1, c[2])
 
+    if args.skip_extra:
+        return res
     # End-to-end Monte Carlo (SURVEY §8 d): each step draws fresh messages,
     # encodes, adds AWGN and decodes on the device, then counts errors.
     ch = AWGNChannel(args.snr)
@@ -289,6 +291,8 @@ def bench_ldpc(args, rank, world):
     _traffic_rate(res["roofline"])
     _valu_rate(res["roofline"], "ldpc_bp_504", torch.cuda.get_device_properties(0).multi_processor_count)
     res["roofline"]["limit"] = "VALU issue (fp64 transcendentals), see roofline.valu; HBM fields are the algorithmic view"
+    if args.skip_extra:
+        return res
     # Second frame source (SURVEY §8 d): valid codewords (all-zero; BP is
     # codeword-symmetric) at the same SNR, early stop on.
     llr0 = AWGNChannel(args.snr).llr_batch_device(None, n, B, seed=4243, frame_offset=rank * B)
@@ -340,6 +344,8 @@ def main():
     ap.add_argument("--cpu-frames-ldpc", type=int, default=65536)
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--skip-ldpc", action="store_true")
+    ap.add_argument("--skip-extra", action="store_true",
+                    help="only the headline decodes (no end-to-end / valid-codeword runs): profiling passes")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -364,7 +370,7 @@ def main():
             "roofline": pol["roofline"],
             "cpu_baseline": pol.get("cpu_baseline"),
             "ber": pol["ber"], "fer": pol["fer"], "plan": pol["plan"],
-            "end_to_end": pol["end_to_end"],
+            "end_to_end": pol.get("end_to_end"),
         }
         if ldp is not None:
             line["ldpc"] = ldp

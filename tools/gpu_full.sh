@@ -14,14 +14,14 @@ timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || 
 echo "bench ok $(date)" >> "$OUT/progress.txt"
 export TMPDIR=/tmp; cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 "$R/bench.py" --skip-cpu > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err" || exit $?
+    python3 "$R/bench.py" --skip-cpu --skip-extra > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err" || exit $?
 echo "trace ok $(date)" >> "$OUT/progress.txt"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-    python3 "$R/bench.py" --skip-cpu > /dev/null 2> "$OUT/pmc_fetch.err" || exit $?
+    python3 "$R/bench.py" --skip-cpu --skip-extra > /dev/null 2> "$OUT/pmc_fetch.err" || exit $?
 echo "fetch ok $(date)" >> "$OUT/progress.txt"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-    python3 "$R/bench.py" --skip-cpu > /dev/null 2> "$OUT/pmc_write.err" || exit $?
+    python3 "$R/bench.py" --skip-cpu --skip-extra > /dev/null 2> "$OUT/pmc_write.err" || exit $?
 echo "write ok $(date)" >> "$OUT/progress.txt"
 timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d "$OUT/pmc_valu" -o run -- \
-    python3 "$R/bench.py" --skip-cpu > /dev/null 2> "$OUT/pmc_valu.err" || exit $?
+    python3 "$R/bench.py" --skip-cpu --skip-extra > /dev/null 2> "$OUT/pmc_valu.err" || exit $?
 echo "valu ok $(date)" >> "$OUT/progress.txt"

@@ -87,6 +87,12 @@ struct TG {
     }
     // byte offset of the beta pool of multi-word depth d (1..NB); word w of slot s at + (w*64 + s)*4
     static constexpr int64_t bl_off(int d) { return W_BL + 8LL * ((1LL << n) - (1LL << (n - d + 1))); }
+    // Shadow lanes + slot-major lane columns (kernel comment at `plane`): on for
+    // every instance but LCAP = 16, where they measured slower (7.3 against
+    // 6.8 ms at N = 1024); there inactive slots keep their own state and planes
+    // and the columns are frame-major, as before.
+    static constexpr bool SHADOW = LCAP != 16;
+    static PL_DEV int pl(int s, int f) { return SHADOW ? s * FPW + f : f * LCAP + s; }
 };
 
 PL_DEV int field(uint64_t row, int d) { return (int)((row >> (RB * d)) & 31u); }
@@ -290,7 +296,7 @@ PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, in
     for (int d = 1; d <= F; ++d) {
         right[d] = (i >> (n - d)) & 1;
         bsrc[d] = reinterpret_cast<const uint32_t*>(ws + G::bl_off(d <= G::NB ? d : 1)) +
-                  field(brow, d) * G::FPW + fw;
+                  G::pl(field(brow, d), fw);
         bw[d] = (d > G::NB) ? beta_get<n>(d, bb, bw5) : 0u;
     }
     if constexpr (G::NS >= 3) {
@@ -344,7 +350,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
     uint64_t* const rowx = reinterpret_cast<uint64_t*>(smem + G::L_ROW + fw * G::GS);  // [LCAP][2]
     uint64_t* const brx = reinterpret_cast<uint64_t*>(smem + G::L_BR) + base;          // [LCAP]
     uint32_t* const surv = reinterpret_cast<uint32_t*>(smem + G::L_SURV) + base;       // [LCAP]
-    uint32_t* const walk0 = reinterpret_cast<uint32_t*>(ws + G::W_WALK) + fw;           // [2][CW][64]
+    uint32_t* const walk0 = reinterpret_cast<uint32_t*>(ws + G::W_WALK) + (G::SHADOW ? fw : 0);  // [2][CW][64]
 
     unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tprev = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
@@ -388,7 +394,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 }
             }
         }
-        uint64_t lrow = 0, brow = 0;  // slot 0's own rows; the other lanes shadow it
+        uint64_t lrow = G::SHADOW ? 0 : own, brow = lrow;  // shadows start on slot 0's rows
         uint32_t bb = 0, bw5 = 0;
         double pm = (slot == 0) ? 0.0 : -INFINITY;
         int nact = 1;
@@ -398,21 +404,21 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         for (int i = 0; i < N; ++i) {
             // ================================================ LLRs down to leaf i
             const int dstart = (i == 0) ? 1 : n - __builtin_ctz(i);
-            const int pslot = slot < nact ? slot : 0;  // shadows use slot 0's planes
-            const int plane = pslot * FPW + fw;
+            const int pslot = (!G::SHADOW || slot < nact) ? slot : 0;  // shadows use slot 0's planes
+            const int plane = G::pl(pslot, fw);
             double lam;
             if (dstart <= DL) ws_sync();  // workspace written by other lanes
             STAMP(7);
             if (dstart <= F) {
                 lam = descend_fused<G>(smem, ws, lane, fw, plane, i, ch, brow, bb, bw5);
-                lrow = set_range(lrow, slot < nact ? own : 0ull, F, n);
+                lrow = set_range(lrow, (!G::SHADOW || slot < nact) ? own : 0ull, F, n);
                 STAMP(0);
             } else {
                 const int p = dstart - 1;
-                const int ps = field(lrow, p) * FPW + fw;
-                const int bs = field(brow, dstart <= G::NB ? dstart : 0) * FPW + fw;
+                const int ps = G::pl(field(lrow, p), fw);
+                const int bs = G::pl(field(brow, dstart <= G::NB ? dstart : 0), fw);
                 lam = descend_from<G, F>(p, smem, ws, plane, ps, bs, bb, bw5);
-                lrow = set_range(lrow, slot < nact ? own : 0ull, dstart, n);
+                lrow = set_range(lrow, (!G::SHADOW || slot < nact) ? own : 0ull, dstart, n);
                 if (p < DL) { STAMP(1); } else { STAMP(2); }
             }
 
@@ -506,7 +512,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     }
                 }
                 lds_sync();
-                {
+                if (G::SHADOW || slot < nsurv) {
                     // survivor `slot` (decoder.py:323-336); lanes beyond the
                     // survivors shadow survivor 0 (see `plane`) with metric -inf
                     const uint32_t e = surv[slot < nsurv ? slot : 0];
@@ -519,6 +525,9 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     const uint64_t br = brx[par];
                     bb = (uint32_t)br;
                     bw5 = (uint32_t)(br >> 32);
+                } else {
+                    pm = -INFINITY;  // LCAP = 16: inactive slots keep their own state
+                    bit = 0;
                 }
                 nact = nsurv;
                 lds_sync();  // scratch reads done before the next leaf's writes
@@ -544,18 +553,18 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     // dd == n-5, cur = one word: multi-word combine through the workspace.
                     // Planes from the list size after this leaf's pruning: a lane that
                     // just stopped shadowing slot 0 writes its own.
-                    const int wslot = slot < nact ? slot : 0;
-                    uint32_t* const walkw = walk0 + wslot * FPW;
+                    const int wslot = (!G::SHADOW || slot < nact) ? slot : 0;
+                    uint32_t* const walkw = walk0 + (G::SHADOW ? wslot * FPW : lane);
                     int parity = 0;
                     ws_sync();  // multi-word betas of other lanes live in the workspace
                     walkw[0] = cur;
                     for (; k < steps; ++k) {
                         const int cwc = 1 << (k - 5);
-                        const int ls = field(brow, dd <= G::NB ? dd : 0) * FPW + fw;
+                        const int ls = G::pl(field(brow, dd <= G::NB ? dd : 0), fw);
                         const bool last = (k + 1 == steps);
                         const uint32_t* lsrc = reinterpret_cast<const uint32_t*>(ws + G::bl_off(dd <= G::NB ? dd : 1)) + ls;
                         uint32_t* ldst = reinterpret_cast<uint32_t*>(ws + G::bl_off(dd - 1 >= 1 ? dd - 1 : 1)) +
-                                         wslot * FPW + fw;
+                                         G::pl(wslot, fw);
                         for (int w = 0; w < 2 * cwc; ++w) {
                             const uint32_t cwv = walkw[(parity * G::CW + (w >> 1)) * 64];
                             const uint32_t lw = (dd > G::NB) ? bw5 : lsrc[(w >> 1) * 64];
@@ -576,7 +585,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         }
 
         // ================================================ best path, output
-        uint32_t* const walk = walk0 + (slot < nact ? slot : 0) * FPW;
+        uint32_t* const walk = walk0 + (G::SHADOW ? (slot < nact ? slot : 0) * FPW : lane);
         int best = 0;
         if constexpr (!SC) {
             met[slot] = make_double2(pm, 0.0);

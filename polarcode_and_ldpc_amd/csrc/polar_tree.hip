@@ -41,6 +41,10 @@ namespace pl {
 
 namespace {
 
+#ifndef RANK_STRICT_LCAP
+#define RANK_STRICT_LCAP 8  // list capacities ranked with strict comparisons
+#endif
+
 constexpr int RB = 5;  // bits per slot field of a pointer row (list capacity <= 32)
 
 template <int NL, int LCAP_, int F_, int DL_>
@@ -468,14 +472,14 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 const int nsurv = (2 * nact < Lsz) ? 2 * nact : Lsz;
                 const uint32_t id0 = (uint32_t)(slot << 1), id1 = id0 | 1u;
                 int r0, r1;
-                if constexpr (LCAP >= 16 || NL >= 11) {
-                    // Large lists / long codes: strict comparisons only -- exact unless two
+                if constexpr (LCAP >= RANK_STRICT_LCAP || NL >= 11) {
+                    // Lists of 8+ / long codes: strict comparisons only -- exact unless two
                     // candidates tie (inactive slots publish -inf and never
                     // count).  A tie makes two candidates claim one survivor
                     // slot; the loser sees it and the wave redoes the ranks with
                     // the stable tie-break.  (L = 32: 9.1 -> 7.5 ms, L = 16:
-                    // 7.7 -> 7.0 ms, N = 2048 / 4096 L = 8: ~2 %; at N = 1024,
-                    // L <= 8 the check costs more than it saves.)
+                    // 7.7 -> 7.0 ms, N = 2048 / 4096 L = 8: ~2 %, N = 1024 L = 8
+                    // with shadow lanes: 6.72 -> 6.54 ms.)
                     r0 = 0;
                     r1 = 0;
                     for (int q0 = 0; q0 < nact; q0 += QC) {

@@ -356,3 +356,29 @@ def test_list_growth_at_multiword_walks(gpu, oracle, N, L):
     want = oracle.scl_decode(N, L, fr, llr, threads=8)
     got = P.SCLDecoder(N, K, list_size=L, frozen_bits=fr).decode_batch(llr)
     assert _mismatch(got, want) == 0
+
+
+@pytest.mark.parametrize("L", [3, 5, 6, 7, 12, 20])
+def test_tree_list_sizes_below_capacity(gpu, oracle, L):
+    """List sizes that are not a power of two run on the tree kernel of the next
+    capacity (8, 16, 32): the extra lanes never become paths (with shadow lanes
+    they follow slot 0 for the whole frame).  Noisy N=1024 frames vs the
+    oracle, bit-exact."""
+    from polarcode_and_ldpc_amd import _native
+    P = _P()
+    N, K = 1024, 512
+    fr = P.construct_frozen_set(N, K, 1.5)
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    rng = np.random.RandomState(100 + L)
+    B = 24
+    snr = rng.uniform(0.0, 2.5, size=(B, 1))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+    msg = rng.randint(0, 2, (B, K))
+    cw = P.PolarEncoder(N, K, frozen_bits=fr).encode_batch(msg)
+    llr = 2.0 * ((1.0 - 2.0 * cw) + sigma * rng.randn(B, N)) / sigma ** 2
+    plan = _native.polar_plan(N, K, mask, L)
+    assert plan.info.reserved == 4  # tree kernel
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    plan.decode(torch.from_numpy(llr).cuda(), out)
+    assert _mismatch(out.cpu().numpy(), oracle.scl_decode(N, L, fr, llr, threads=8)) == 0

@@ -196,7 +196,7 @@ PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int plane, int p
 // depth-d ancestor of leaf i is a right child), then the f-chain to the leaf.
 template <class G, int D0>
 PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int fw, int plane, const double* ch,
-                         const bool* right, const uint32_t* const* bsrc, uint32_t* bw) {
+                         const double2* raw, const bool* right, const uint32_t* const* bsrc, uint32_t* bw) {
     constexpr int n = G::n, F = G::F, SF = 1 << (n - F), W = 1 << (F - D0);
     Fold<G> st;
     st.lam = 0.0;
@@ -211,11 +211,16 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
         // its frame's pairs back as LDS broadcasts.  Next chunk prefetched.
         constexpr int CH = 1;  // pairs per lane per chunk (CH = 2: 7.5 ms against 7.06)
         constexpr int PPI = W / 2, IPC = CH * G::LCAP / PPI, NCH = SF / IPC;
-        const double2* src = reinterpret_cast<const double2*>(ws + G::st_off(D0));
+        // depth 0 straight from the input rows when they are 16-byte aligned
+        // (`raw`: pair lane / FPW of frame lane % FPW; chunk c at + c * LCAP):
+        // the same 8 lines per chunk as the staged copy, which is then not stored
+        const bool from_raw = D0 == 0 && raw != nullptr;
+        const double2* src = from_raw ? raw : reinterpret_cast<const double2*>(ws + G::st_off(D0)) + lane;
+        const int cstr = from_raw ? G::LCAP : 64;
         double2* stg = reinterpret_cast<double2*>(smem + G::L_MET);
         double2 nxt[CH];
 #pragma unroll
-        for (int h = 0; h < CH; ++h) nxt[h] = src[h * 64 + lane];
+        for (int h = 0; h < CH; ++h) nxt[h] = src[h * cstr];
 #pragma unroll 1
         for (int c = 0; c < NCH; ++c) {
             lds_sync();  // the previous chunk's reads are issued before the overwrite
@@ -223,7 +228,7 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
             for (int h = 0; h < CH; ++h) stg[h * 64 + lane] = nxt[h];
             if (c + 1 < NCH) {
 #pragma unroll
-                for (int h = 0; h < CH; ++h) nxt[h] = src[((c + 1) * CH + h) * 64 + lane];
+                for (int h = 0; h < CH; ++h) nxt[h] = src[((c + 1) * CH + h) * cstr];
             }
             lds_sync();
 #pragma unroll 2
@@ -291,7 +296,7 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
 
 template <class G>
 PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, int fw, int plane, int i,
-                            const double* ch, uint64_t brow, uint32_t bb, uint32_t bw5) {
+                            const double* ch, const double2* raw, uint64_t brow, uint32_t bb, uint32_t bw5) {
     constexpr int n = G::n, F = G::F;
     bool right[F + 1];
     const uint32_t* bsrc[F + 1];
@@ -304,15 +309,15 @@ PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, in
         bw[d] = (d > G::NB) ? beta_get<n>(d, bb, bw5) : 0u;
     }
     if constexpr (G::NS >= 3) {
-        if (!right[1] && !right[2] && !right[3]) return fused_loop<G, 3>(smem, ws, lane, fw, plane, ch, right, bsrc, bw);
+        if (!right[1] && !right[2] && !right[3]) return fused_loop<G, 3>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw);
     }
     if constexpr (G::NS >= 2) {
-        if (!right[1] && !right[2]) return fused_loop<G, 2>(smem, ws, lane, fw, plane, ch, right, bsrc, bw);
+        if (!right[1] && !right[2]) return fused_loop<G, 2>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw);
     }
     if constexpr (G::NS >= 1) {
-        if (!right[1]) return fused_loop<G, 1>(smem, ws, lane, fw, plane, ch, right, bsrc, bw);
+        if (!right[1]) return fused_loop<G, 1>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw);
     }
-    return fused_loop<G, 0>(smem, ws, lane, fw, plane, ch, right, bsrc, bw);
+    return fused_loop<G, 0>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw);
 }
 
 template <class G, int P>
@@ -369,6 +374,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         const int64_t frame = f0 + fw;
         const bool live = frame < batch;
         const double* __restrict__ ch = llr + (live ? frame : batch - 1) * ld;
+        const double2* raw = nullptr;  // depth-0 pairs read in place (fused_loop)
         if constexpr (G::STAGE) {
             // channel rows of this wave's frames -> [N/2][FPW] pairs, plus the
             // path-independent left-most f-only nodes of depths 1..NS.
@@ -376,6 +382,8 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
             const int sf = lane % FPW;
             const int64_t fr = f0 + sf < batch ? f0 + sf : batch - 1;
             const double* row = llr + fr * ld;
+            if (G::n <= 10 && G::LCAP >= (1 << G::F) / 2 && (ld & 1) == 0 && ((uintptr_t)llr & 15) == 0)
+                raw = reinterpret_cast<const double2*>(row) + lane / FPW;
             constexpr int CV = 2 << G::NS;    // channel values per lane per step
             constexpr int CPI = 64 / FPW;     // chunks per frame per step
 #pragma unroll 1
@@ -389,8 +397,10 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 for (int d = 0; d <= G::NS; ++d) {
                     double2* dst = reinterpret_cast<double2*>(ws + G::st_off(d)) + sf;
                     const int np = CV >> (d + 1);
+                    if (d > 0 || raw == nullptr) {
 #pragma unroll
-                    for (int k = 0; k < np; ++k) dst[(np * cc + k) * FPW] = make_double2(v[2 * k], v[2 * k + 1]);
+                        for (int k = 0; k < np; ++k) dst[(np * cc + k) * FPW] = make_double2(v[2 * k], v[2 * k + 1]);
+                    }
                     if (d < G::NS) {
 #pragma unroll
                         for (int k = 0; k < np; ++k) v[k] = f_ms(v[2 * k], v[2 * k + 1]);
@@ -414,7 +424,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
             if (dstart <= DL) ws_sync();  // workspace written by other lanes
             STAMP(7);
             if (dstart <= F) {
-                lam = descend_fused<G>(smem, ws, lane, fw, plane, i, ch, brow, bb, bw5);
+                lam = descend_fused<G>(smem, ws, lane, fw, plane, i, ch, raw, brow, bb, bw5);
                 lrow = set_range(lrow, (!G::SHADOW || slot < nact) ? own : 0ull, F, n);
                 STAMP(0);
             } else {

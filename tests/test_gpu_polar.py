@@ -382,3 +382,24 @@ def test_tree_list_sizes_below_capacity(gpu, oracle, L):
     out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
     plan.decode(torch.from_numpy(llr).cuda(), out)
     assert _mismatch(out.cpu().numpy(), oracle.scl_decode(N, L, fr, llr, threads=8)) == 0
+
+
+@pytest.mark.parametrize("pad,off", [(0, 0), (1, 0), (2, 0), (6, 1)])
+def test_strided_and_unaligned_rows(gpu, pad, off):
+    """Channel rows with a leading dimension N + pad and a base offset of `off`
+    doubles: the tree kernel reads depth-0 pairs in place only for 16-byte
+    aligned rows (even ld, aligned base) and stages them otherwise; both give
+    the contiguous decode's bits."""
+    from polarcode_and_ldpc_amd import _native
+    d = golden("polar_scl_1024_l8.npz")
+    mask = np.zeros(1024, np.uint8)
+    mask[d["frozen"]] = 1
+    plan = _native.polar_plan(1024, 512, mask, 8)
+    llr = torch.from_numpy(d["llr"]).cuda()
+    B = llr.shape[0]
+    buf = torch.full((B * (1024 + pad) + off + 8,), float("nan"), dtype=torch.float64, device="cuda")
+    view = buf[off:off + B * (1024 + pad)].view(B, 1024 + pad)[:, :1024]
+    view.copy_(llr)
+    out = torch.empty((B, 512), dtype=torch.uint8, device="cuda")
+    plan.decode(view, out)
+    assert _mismatch(out.cpu().numpy(), d["scl"]) == 0

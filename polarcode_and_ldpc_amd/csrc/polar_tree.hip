@@ -19,8 +19,9 @@
 //     counter order).  Every depth is stored once, as 16-byte pairs, for the
 //     later g of its right sibling; no depth is re-read by its left child;
 //   * tiers by depth, offsets compile-time constants:
-//       depth 0        channel LLRs, staged per wave transposed [N/2][frames]
-//                      (a frame's lanes share each load: one line per load),
+//       depth 0        channel LLRs: read in place from aligned input rows by
+//                      the de-duplicated fused top (n <= 10), else staged per
+//                      wave transposed [N/2][frames] (one line per load),
 //       depths 1..F-1  recomputed from the channel (fused top),
 //       depths F..DL-1 per-wave global workspace, [S/2][64 lanes] f64 pairs,
 //       depths DL..n-1 LDS, same pair-interleaved layout,
@@ -30,7 +31,10 @@
 //     the LLR pools.  A list clone copies 24 bytes (rows + beta registers);
 //   * pruning runs through LDS: lanes publish (m0, m1) and rows, read their
 //     frame's metrics with 16-byte broadcasts (group stride padded against bank
-//     conflicts), rank, and scatter survivors to a slot table.
+//     conflicts), rank, and scatter survivors to a slot table;
+//   * lane columns are slot-major and, while the list grows, lanes beyond the
+//     active paths shadow slot 0 (TG::SHADOW), so inactive paths cost no memory
+//     traffic.
 #include "common.hpp"
 #include "internal.hpp"
 #include "polar_common.hpp"

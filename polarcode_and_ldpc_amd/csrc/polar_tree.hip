@@ -701,6 +701,14 @@ const TreeEntry* tree_table(int* count) {
         make_entry<10, 4, false, 3, 7>(),
         make_entry<11, 8, false, 3, 8>(),
         make_entry<12, 8, false, 3, 9>(),
+        make_entry<8, 2, false, 3, 5>(),
+        make_entry<8, 4, false, 3, 5>(),
+        make_entry<8, 8, false, 3, 5>(),
+        make_entry<8, 16, false, 3, 5>(),
+        make_entry<8, 32, false, 3, 5>(),
+        make_entry<9, 8, false, 3, 6>(),
+        make_entry<9, 16, false, 3, 6>(),
+        make_entry<10, 2, false, 3, 7>(),
         make_entry<8, 1, true, 3, 5>(),
         make_entry<9, 1, true, 3, 6>(),
         make_entry<10, 1, true, 3, 7>(),

@@ -403,3 +403,29 @@ def test_strided_and_unaligned_rows(gpu, pad, off):
     out = torch.empty((B, 512), dtype=torch.uint8, device="cuda")
     plan.decode(view, out)
     assert _mismatch(out.cpu().numpy(), d["scl"]) == 0
+
+
+@pytest.mark.parametrize("N,L", [(256, 2), (256, 4), (256, 8), (256, 16), (256, 32), (512, 8), (512, 16),
+                                 (1024, 2)])
+def test_small_code_tree_instances_vs_oracle(gpu, oracle, N, L):
+    """Tree-kernel instances for N = 256 / 512 and L = 2 (the reference's
+    sc_vs_scl / benchmark_scl sizes): noisy frames vs the oracle, bit-exact."""
+    from polarcode_and_ldpc_amd import _native
+    P = _P()
+    K = N // 2
+    fr = P.construct_frozen_set(N, K, 1.0)
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    rng = np.random.RandomState(7 * N + L)
+    B = 40
+    snr = rng.uniform(-0.5, 3.0, size=(B, 1))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+    msg = rng.randint(0, 2, (B, K))
+    cw = P.PolarEncoder(N, K, frozen_bits=fr).encode_batch(msg)
+    llr = 2.0 * ((1.0 - 2.0 * cw) + sigma * rng.randn(B, N)) / sigma ** 2
+    llr[0, ::9] = 0.0  # erasures: metric ties
+    plan = _native.polar_plan(N, K, mask, L)
+    assert plan.info.reserved == 4  # tree kernel
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    plan.decode(torch.from_numpy(llr).cuda(), out)
+    assert _mismatch(out.cpu().numpy(), oracle.scl_decode(N, L, fr, llr, threads=8)) == 0

@@ -7,8 +7,11 @@ from polarcode_and_ldpc_amd import _native
 from polarcode_and_ldpc_amd.channel import AWGNChannel
 from polarcode_and_ldpc_amd.polar import construct_frozen_set
 
-for N, L, B in [(256, 0, 65536), (1024, 0, 65536), (4096, 0, 65536), (1024, 4, 65536), (1024, 8, 65536),
-                (2048, 8, 32768), (1024, 16, 32768), (1024, 32, 16384), (4096, 8, 16384)]:
+CONFIGS = [(256, 0, 65536), (1024, 0, 65536), (4096, 0, 65536), (1024, 4, 65536), (1024, 8, 65536),
+           (2048, 8, 32768), (1024, 16, 32768), (1024, 32, 16384), (4096, 8, 16384)]
+if len(sys.argv) > 1:  # e.g. "256:8:65536,512:8:65536"
+    CONFIGS = [tuple(int(x) for x in c.split(":")) for c in sys.argv[1].split(",")]
+for N, L, B in CONFIGS:
     K = N // 2
     fr = construct_frozen_set(N, K, 2.0)
     mask = np.zeros(N, np.uint8); mask[fr] = 1

@@ -100,6 +100,14 @@ struct TG {
     // 6.8 ms at N = 1024); there inactive slots keep their own state and planes
     // and the columns are frame-major, as before.
     static constexpr bool SHADOW = LCAP != 16;
+    // fused top from staged depth D0 with de-duplicated chunk reads: a chunk is
+    // LCAP pairs of every frame, W / 2 = 2^(F-D0-1) of them per depth-F
+    // element, and the depth-F array (2^(n-F) elements) must fill at least one
+    // chunk; n <= 10 only (at N = 2048 / 4096, L = 8 it measured slower, 8.7 /
+    // 13.0 ms against 8.3 / 12.0)
+    static constexpr bool dedup(int D0) {
+        return STAGE && n <= 10 && LCAP >= (1 << (F - D0)) / 2 && (1 << (n - F)) * ((1 << (F - D0)) / 2) >= LCAP;
+    }
     static PL_DEV int pl(int s, int f) { return SHADOW ? s * FPW + f : f * LCAP + s; }
 };
 
@@ -204,9 +212,7 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
     constexpr int n = G::n, F = G::F, SF = 1 << (n - F), W = 1 << (F - D0);
     Fold<G> st;
     st.lam = 0.0;
-    // (n <= 10: at N = 2048 / 4096, L = 8 it measured slower, 8.7 / 13.0 ms
-    // against 8.3 / 12.0)
-    if constexpr (G::STAGE && G::LCAP >= W / 2 && G::n <= 10) {
+    if constexpr (G::dedup(D0)) {
         // De-duplicated staged reads: the staged depth is [S/2][FPW] pairs, so
         // a 1 KB chunk (LCAP pairs of every frame of the wave) is contiguous.
         // Each lane fetches one distinct 16-byte pair of it (instead of the
@@ -386,7 +392,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
             const int sf = lane % FPW;
             const int64_t fr = f0 + sf < batch ? f0 + sf : batch - 1;
             const double* row = llr + fr * ld;
-            if (G::n <= 10 && G::LCAP >= (1 << G::F) / 2 && (ld & 1) == 0 && ((uintptr_t)llr & 15) == 0)
+            if (G::dedup(0) && (ld & 1) == 0 && ((uintptr_t)llr & 15) == 0)
                 raw = reinterpret_cast<const double2*>(row) + lane / FPW;
             constexpr int CV = 2 << G::NS;    // channel values per lane per step
             constexpr int CPI = 64 / FPW;     // chunks per frame per step
@@ -709,6 +715,9 @@ const TreeEntry* tree_table(int* count) {
         make_entry<9, 8, false, 3, 6>(),
         make_entry<9, 16, false, 3, 6>(),
         make_entry<10, 2, false, 3, 7>(),
+        make_entry<7, 8, false, 3, 4>(),
+        make_entry<7, 32, false, 3, 4>(),
+        make_entry<7, 1, true, 3, 4>(),
         make_entry<8, 1, true, 3, 5>(),
         make_entry<9, 1, true, 3, 6>(),
         make_entry<10, 1, true, 3, 7>(),

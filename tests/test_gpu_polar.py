@@ -429,3 +429,29 @@ def test_small_code_tree_instances_vs_oracle(gpu, oracle, N, L):
     out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
     plan.decode(torch.from_numpy(llr).cuda(), out)
     assert _mismatch(out.cpu().numpy(), oracle.scl_decode(N, L, fr, llr, threads=8)) == 0
+
+
+@pytest.mark.parametrize("L", [0, 8, 32])
+def test_n128_tree_instances_vs_oracle(gpu, oracle, L):
+    """N = 128 (the reference's throughput_test default size) on the tree
+    kernel: SC and SCL L = 8 / 32 against the oracle, bit-exact."""
+    from polarcode_and_ldpc_amd import _native
+    P = _P()
+    N, K = 128, 64
+    fr = P.construct_frozen_set(N, K, 1.0)
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    rng = np.random.RandomState(128 + L)
+    B = 48
+    snr = rng.uniform(-1.0, 3.0, size=(B, 1))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+    msg = rng.randint(0, 2, (B, K))
+    cw = P.PolarEncoder(N, K, frozen_bits=fr).encode_batch(msg)
+    llr = 2.0 * ((1.0 - 2.0 * cw) + sigma * rng.randn(B, N)) / sigma ** 2
+    llr[1, ::5] = 0.0
+    plan = _native.polar_plan(N, K, mask, L)
+    assert plan.info.reserved == 4  # tree kernel
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    plan.decode(torch.from_numpy(llr).cuda(), out)
+    want = oracle.sc_decode(N, fr, llr, threads=8) if L == 0 else oracle.scl_decode(N, L, fr, llr, threads=8)
+    assert _mismatch(out.cpu().numpy(), want) == 0

@@ -4,19 +4,34 @@
 Headline (`value`): Polar N=1024 K=512 SCL L=8, 65 536 AWGN frames per GPU
 (BASELINE.json configs[1]); a step = one batched decode of the resident LLR
 matrix + on-device error count (+ one all-reduce of the counters when N > 1).
-Secondary (`ldpc`): LDPC (504,252) BP max_iter=20 (configs[2]) on the
-reference harness's frames (benchmarks/throughput_test.py:285-315: its encoder's
-invalid codewords, so every frame runs all 20 iterations); `ldpc.valid_codewords`
-is the same decode on valid (all-zero) codewords with early stop.
-`end_to_end`: the polar Monte-Carlo step with fresh device messages, encoding and
-AWGN inside the timed region (SURVEY §8 d "end-to-end MC").
+Secondary keys, each with its own roofline:
+  `ldpc`       LDPC (504,252) BP max_iter=20 (configs[2]) on the reference
+               harness's frames (benchmarks/throughput_test.py:285-315: its
+               encoder's invalid codewords, so every frame runs 20 iterations);
+               `ldpc.valid_codewords`: all-zero codewords with early stop;
+  `end_to_end` the polar Monte-Carlo step with fresh device messages, encoding
+               and AWGN inside the timed region (SURVEY §8 d);
+  `cascl_l32`  CA-SCL N=1024 K=512 L=32 + CRC-8 (configs[3]) decode throughput
+               and a -2..5 dB BER/FER sweep through harness.ber (max_errors stop,
+               frames sharded over the ranks);
+  `long_block` configs[4] per GPU (1 M frames / 8): polar N=4096 K=2048 SCL L=8
+               and LDPC n=8192 (3,6)-regular min-sum, 131 072 frames each.
+`cpu_baseline`: the reference's NumPy decode loops restated (oracle/refnumpy.py,
+bit-exact with the reference fixtures) over a spawn pool of host processes on the
+first frames of the same LLR batch; the C port (oracle/refcpu.c, OpenMP) beside it.
 
 info-Mbps = frames * K_info / t / 1e6 (throughput_test.py:217, :304).
-Usage: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torchrun.
+Usage: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no
+WORLD_SIZE in the environment, bench.py re-launches itself under
+torch.distributed.run with N ranks (before any GPU call).  `--cpu-stub` runs the
+same rank/timing/all-reduce path on CPU (gloo) with a stub decode: a plumbing
+check, never a measurement.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,36 +44,84 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decoded info-Mbps: polar N=1024 SCL L=8 & LDPC(504,252) BP, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+CLOCK_GHZ = 2.4
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def timed_steps(step, steps, warmup, world):
+# ---------------------------------------------------------------- ranks
+class Runtime:
+    """One process per GPU (RCCL) or, with --cpu-stub, per CPU rank (gloo)."""
+
+    def __init__(self, stub: bool):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.stub = stub
+        if stub:
+            self.device = torch.device("cpu")
+            if self.world > 1:
+                dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(self.local)
+            self.device = torch.device("cuda", self.local)
+            if self.world > 1:
+                dist.init_process_group("nccl", device_id=self.device)
+
+    def sync(self):
+        if not self.stub:
+            torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def all_reduce(self, t, op=None):
+        if self.world > 1:
+            dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
+        return t
+
+    def gather(self, x: float):
+        """x from every rank, rank order."""
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        if self.world == 1:
+            return [x]
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t)
+        return [float(o.item()) for o in out]
+
+    def close(self):
+        if self.world > 1:
+            dist.destroy_process_group()
+
+
+def timed_steps(step, steps, warmup, rt, on_timed=None):
+    """W untimed warmup steps, then EXACTLY `steps` steps bracketed by barrier +
+    device synchronisation on both sides.  Returns (max over ranks, per-rank)."""
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    rt.sync()
+    rt.barrier()
+    rt.sync()
+    if on_timed is not None:
+        on_timed()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    rt.sync()
+    rt.barrier()
+    rt.sync()
     dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    return dt
+    per_rank = rt.gather(dt)
+    return max(per_rank), per_rank
 
 
 class KernelTimer:
-    """HIP events around the decode launch, on the stream it is launched on."""
+    """HIP events around each decode launch, on the stream it is launched on
+    (the decoders launch on torch's current stream); reset when the timed
+    region starts, so the mean covers exactly the timed launches."""
 
     def __init__(self):
         self.pairs = []
@@ -78,169 +141,184 @@ class KernelTimer:
         return float(np.mean([s.elapsed_time(e) for s, e in self.pairs])) if self.pairs else float("nan")
 
 
-def load_traffic(name):
+# ---------------------------------------------------------------- roofline
+def _pmc(name):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
     try:
-        t = json.load(open(p)).get(name)
-        return None if t is None else float(t["bytes_per_launch"])
+        return json.load(open(p)).get(name)
     except Exception:
         return None
 
 
-def load_valu(name):
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        return float(json.load(open(p))[name]["valu_instr_per_launch"])
-    except Exception:
-        return None
+def roofline(name, kernel, frames, bytes_per_frame, kms):
+    """Algorithmic bytes per launch / live kernel time against HBM peak, plus the
+    PMC figures for the same kernel from profiles/pmc_traffic.json: HBM-side
+    traffic per launch (2*FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md gfx950
+    correction) and the VALU issue rate against the SIMD-32 ceiling (a wave64
+    fp64 VALU instruction occupies a SIMD 4 cycles, any other VALU 2 cycles:
+    MI355X_MICROARCH.md:53-54 and the 78.6 / 157.3 TF fp64 / fp32 vector peaks)."""
+    achieved = frames * bytes_per_frame / (kms / 1e3) / 1e9
+    r = dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s", frac=achieved / HBM_PEAK_GBS,
+             traffic=None, algorithmic_bytes_per_frame=bytes_per_frame, frames_per_launch=frames, kernel=kernel,
+             kernel_ms=kms)
+    p = _pmc(name)
+    if not p:
+        return r
+    r["traffic"] = float(p["bytes_per_launch"]) * frames / float(p.get("frames", frames))
+    r["traffic_unit"] = "HBM-side bytes per launch (2*FETCH_SIZE+WRITE_SIZE, rocprofv3 PMC)"
+    r["traffic_source"] = p.get("source")
+    r["traffic_GBps"] = r["traffic"] / (kms / 1e3) / 1e9
+    r["traffic_frac"] = r["traffic_GBps"] / HBM_PEAK_GBS
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    if "valu_fp64_per_launch" in p and "valu_per_launch" in p:
+        scale = frames / float(p.get("frames", frames))
+        f64 = float(p["valu_fp64_per_launch"]) * scale
+        other = max(0.0, float(p["valu_per_launch"]) * scale - f64)
+        # SIMD-cycles needed at full issue / SIMD-cycles available in the launch
+        need = 4.0 * f64 + 2.0 * other
+        avail = cus * 4 * CLOCK_GHZ * 1e9 * kms / 1e3
+        r["valu"] = dict(fp64_instr=f64, other_instr=other, simd_cycles_needed=need, simd_cycles_available=avail,
+                         frac=need / avail, ceiling="4 cyc/wave64 fp64 VALU, 2 cyc other VALU, per SIMD-32; "
+                                                   "%d CUs x 4 SIMDs x %.1f GHz" % (cus, CLOCK_GHZ),
+                         source=p.get("source"))
+    return r
 
 
-def _valu_rate(roof, name, cus, clock_ghz=2.4):
-    """VALU issue against its ceiling: SQ_INSTS_VALU (PMC, per launch) over the
-    live kernel time.  A CU issues at most one wave64 fp64 VALU instruction per
-    cycle (4 SIMDs, 4 cycles each), so peak = CUs x clock."""
-    v = load_valu(name)
-    if v is None:
-        return
-    rate = v / (roof["kernel_ms"] / 1e3) / 1e9  # G wave-instructions / s
-    peak = cus * clock_ghz
-    roof["valu"] = dict(instr_per_launch=v, achieved=rate, peak=peak, unit="G wave-instr/s (fp64 VALU)",
-                        frac=rate / peak, source="profiles/pmc_traffic.json (SQ_INSTS_VALU)")
+# ---------------------------------------------------------------- CPU baseline
+def cpu_processes():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
 
 
-def traffic_source(name):
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        return json.load(open(p))[name]["source"]
-    except Exception:
-        return None
+def numpy_baseline(pool, procs, what, fn, frames, info_bits, gpu_bits):
+    """Time the NumPy restatement of the reference loops on `frames` frames."""
+    t0 = time.perf_counter()
+    bits = fn()
+    ct = time.perf_counter() - t0
+    return dict(value=frames * info_bits / ct / 1e6, unit="info-Mbps", cores=procs, kind="port",
+                sample="first %d frames of the same LLR batch: %s (oracle/refnumpy.py, the reference's NumPy "
+                       "per-frame loops restated, bit-exact with its fixtures), %d spawn processes, %.1f s"
+                       % (frames, what, procs, ct),
+                mismatching_frames_vs_gpu=int((bits != gpu_bits).any(axis=1).sum()))
 
 
-def _traffic_rate(roof):
-    """Measured HBM-side bytes per launch (PMC) over the live kernel time: the
-    bandwidth the kernel actually draws, beside the algorithmic-bytes roofline."""
-    if roof.get("traffic"):
-        gbs = roof["traffic"] / (roof["kernel_ms"] / 1e3) / 1e9
-        roof["traffic_GBps"] = gbs
-        roof["traffic_frac"] = gbs / HBM_PEAK_GBS
-
-
-def cpu_threads():
-    n = len(os.sched_getaffinity(0))
-    return max(1, min(16, n))
-
-
-def bench_polar(args, rank, world):
+# ---------------------------------------------------------------- polar
+def polar_fixture(rt, N, K, L, B, snr, seed, frozen_snr=2.0):
     from polarcode_and_ldpc_amd import _native
     from polarcode_and_ldpc_amd.channel import AWGNChannel
     from polarcode_and_ldpc_amd.polar import SCLDecoder, construct_frozen_set
-
-    N, K, L, B = 1024, 512, args.list_size, args.batch
-    frozen = construct_frozen_set(N, K, 2.0)
+    frozen = construct_frozen_set(N, K, frozen_snr)
     dec = SCLDecoder(N, K, list_size=L, frozen_bits=frozen)
-    plan = dec.plan
-    off = rank * B
+    off = rt.rank * B  # global frame indices: identical frames for any GPU count
     msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
-    _native.random_bits(42, off, msg)
+    _native.random_bits(seed, off, msg)
     cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
-    _native.polar_encode(plan, msg, cw)
-    llr = AWGNChannel(args.snr).llr_batch_device(cw, N, B, seed=42, frame_offset=off)
-    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
-    counts = torch.zeros(3, dtype=torch.int64, device="cuda")
-    kt = KernelTimer()
+    _native.polar_encode(dec.plan, msg, cw)
+    llr = AWGNChannel(snr).llr_batch_device(cw, N, B, seed=seed, frame_offset=off)
+    del cw
+    return dec, frozen, msg, llr
 
-    sc = torch.zeros(3, dtype=torch.int64, device="cuda")  # this step's counters
+
+def polar_kernel_name(plan, n):
+    i = plan.info
+    if i.reserved == 4:
+        return "polar_tree_kernel<n=%d,LCAP=%d,%s,F=%d>" % (n, 64 // max(1, i.frames_per_block),
+                                                          "SC" if i.list_size == 0 else "SCL", i.fused_top)
+    return "polar_lane_kernel (generation %d)" % i.reserved
+
+
+def decode_loop(rt, plan, llr, out, msg, width, steps, warmup, iters=None):
+    """Timed decode + device error count (+ counter all-reduce) steps."""
+    from polarcode_and_ldpc_amd import _native
+    kt = KernelTimer()
+    counts = torch.zeros(3, dtype=torch.int64, device="cuda")
+    sc = torch.zeros(3, dtype=torch.int64, device="cuda")
 
     def step():
-        kt(lambda: plan.decode(llr, out))
+        kt(lambda: plan.decode(llr, out, iters))
         sc.zero_()
-        _native.count_errors(msg, out, K, sc)
-        if world > 1:
-            dist.all_reduce(sc)
+        _native.count_errors(msg, out, width, sc)
+        rt.all_reduce(sc)
         counts.add_(sc)
 
-    dt = timed_steps(step, args.steps, args.warmup, world)
-    kms = kt.mean_ms()  # includes warmup launches; steady state
-    kt.reset()
-    for _ in range(3):
-        kt(lambda: plan.decode(llr, out))
-    kms = kt.mean_ms()
-    frames = B * world * args.steps
-    value = frames * K / dt / 1e6
-    bytes_per_frame = 8 * N + K
-    achieved = B * bytes_per_frame / (kms / 1e3) / 1e9
-    res = dict(value=value, ms_per_step=dt / args.steps * 1e3, kernel_ms=kms, B=B,
-               roofline=dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
-                             frac=achieved / HBM_PEAK_GBS, traffic=load_traffic("polar_scl_1024_l8"),
-                             traffic_unit="HBM bytes per launch (2*FETCH_SIZE+WRITE_SIZE, rocprofv3 PMC)",
-                             traffic_source=traffic_source("polar_scl_1024_l8"),
-                             algorithmic_bytes_per_frame=bytes_per_frame, frames_per_launch=B,
-                             kernel=("polar_tree_kernel<n=10,LCAP=%d,SCL,F=%d>" % (L, plan.info.fused_top)
-                                     if plan.info.reserved == 4 else "polar_lane_kernel (generation %d)"
-                                     % plan.info.reserved),
-                             kernel_ms=kms),
-               plan=dict(lds_bytes=plan.info.lds_bytes, fused_top=plan.info.fused_top))
-    _traffic_rate(res["roofline"])
-    _valu_rate(res["roofline"], "polar_scl_1024_l8", torch.cuda.get_device_properties(0).multi_processor_count)
-    c = counts.cpu().numpy()
-    res["ber"] = float(c[0]) / max(1, c[2] * K)
-    res["fer"] = float(c[1]) / max(1, c[2])
+    def start():
+        kt.reset()
+        counts.zero_()
 
-    if args.skip_extra:
-        return res
-    # End-to-end Monte Carlo (SURVEY §8 d): each step draws fresh messages,
-    # encodes, adds AWGN and decodes on the device, then counts errors.
-    ch = AWGNChannel(args.snr)
-    e2e_counts = torch.zeros(3, dtype=torch.int64, device="cuda")
-    e2e_step_no = [0]
-    msg2, cw2, out2 = torch.empty_like(msg), torch.empty_like(cw), torch.empty_like(out)
-    llr2 = torch.empty_like(llr)
+    dt, per_rank = timed_steps(step, steps, warmup, rt, on_timed=start)
+    return dt, per_rank, kt.mean_ms(), counts.cpu().numpy()
 
-    def e2e_step():
-        o = off + e2e_step_no[0] * B * world  # fresh global frame indices every step
-        e2e_step_no[0] += 1
-        _native.random_bits(43, o, msg2)
-        _native.polar_encode(plan, msg2, cw2)
-        ch.llr_batch_device(cw2, N, B, seed=43, frame_offset=o, out=llr2)
-        plan.decode(llr2, out2)
-        sc.zero_()
-        _native.count_errors(msg2, out2, K, sc)
-        if world > 1:
-            dist.all_reduce(sc)
-        e2e_counts.add_(sc)
 
-    edt = timed_steps(e2e_step, args.steps, args.warmup, world)
-    ec = e2e_counts.cpu().numpy()
-    res["end_to_end"] = dict(value=B * world * args.steps * K / edt / 1e6, unit="info-Mbps",
-                             ms_per_step=edt / args.steps * 1e3,
-                             what="per step: device random messages + polar encode + AWGN LLRs (Philox) + "
-                                  "SCL decode + error count (+ all-reduce)",
-                             ber=float(ec[0]) / max(1, ec[2] * K), fer=float(ec[1]) / max(1, ec[2]))
-    if rank == 0 and world == 1 and not args.skip_cpu:
+def bench_polar(args, rt, pool):
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    N, K, L, B = 1024, 512, args.list_size, args.batch
+    dec, frozen, msg, llr = polar_fixture(rt, N, K, L, B, args.snr, 42)
+    plan = dec.plan
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    dt, per_rank, kms, c = decode_loop(rt, plan, llr, out, msg, K, args.steps, args.warmup)
+    res = dict(value=B * rt.world * args.steps * K / dt / 1e6, ms_per_step=dt / args.steps * 1e3,
+               rank_ms_per_step=[t / args.steps * 1e3 for t in per_rank], kernel_ms=kms, B=B,
+               roofline=roofline("polar_scl_1024_l8", polar_kernel_name(plan, 10), B, 8 * N + K, kms),
+               plan=dict(lds_bytes=plan.info.lds_bytes, fused_top=plan.info.fused_top),
+               ber=float(c[0]) / max(1, c[2] * K), fer=float(c[1]) / max(1, c[2]), frames_counted=int(c[2]))
+
+    if not args.skip_extra:
+        # End-to-end Monte Carlo (SURVEY §8 d): fresh messages, encoding, AWGN,
+        # decode and error count per step, all on the device.
+        ch = AWGNChannel(args.snr)
+        ec = torch.zeros(3, dtype=torch.int64, device="cuda")
+        sc = torch.zeros(3, dtype=torch.int64, device="cuda")
+        stepno = [0]
+        msg2, out2 = torch.empty_like(msg), torch.empty_like(out)
+        cw2 = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+        llr2 = torch.empty_like(llr)
+
+        def e2e_step():
+            o = rt.rank * B + stepno[0] * B * rt.world  # fresh global frame indices every step
+            stepno[0] += 1
+            _native.random_bits(43, o, msg2)
+            _native.polar_encode(plan, msg2, cw2)
+            ch.llr_batch_device(cw2, N, B, seed=43, frame_offset=o, out=llr2)
+            plan.decode(llr2, out2)
+            sc.zero_()
+            _native.count_errors(msg2, out2, K, sc)
+            rt.all_reduce(sc)
+            ec.add_(sc)
+
+        edt, _ = timed_steps(e2e_step, args.steps, args.warmup, rt, on_timed=ec.zero_)
+        e = ec.cpu().numpy()
+        res["end_to_end"] = dict(value=B * rt.world * args.steps * K / edt / 1e6, unit="info-Mbps",
+                                 ms_per_step=edt / args.steps * 1e3,
+                                 what="per step: device random messages + polar encode + AWGN LLRs (Philox) + "
+                                      "SCL decode + error count (+ all-reduce)",
+                                 ber=float(e[0]) / max(1, e[2] * K), fer=float(e[1]) / max(1, e[2]))
+        del msg2, out2, cw2, llr2
+
+    if pool is not None:
         from oracle import oracle as O
-        S = args.cpu_frames
-        th = cpu_threads()
-        llr_h = llr[:S].cpu().numpy()
+        from oracle import refnumpy as R
+        S = args.cpu_frames_numpy
+        llr_h = llr[:max(S, args.cpu_frames)].cpu().numpy()
+        got = out[:llr_h.shape[0]].cpu().numpy().astype(np.int64)
+        procs = cpu_processes()
+        res["cpu_baseline"] = numpy_baseline(
+            pool, procs, "SCL N=1024 L=%d" % L,
+            lambda: R.polar_batch(N, L, frozen, llr_h[:S], pool=pool), S, K, got[:S])
+        S2 = args.cpu_frames
         t0 = time.perf_counter()
-        ref = O.scl_decode(N, L, frozen, llr_h, threads=th)
+        ref = O.scl_decode(N, L, frozen, llr_h[:S2], threads=procs)
         ct = time.perf_counter() - t0
-        got = out[:S].cpu().numpy().astype(np.int64)
-        res["cpu_baseline"] = dict(value=S * K / ct / 1e6, unit="info-Mbps", cores=th, kind="port",
-                                   sample="first %d frames of the same LLR batch, oracle/refcpu.c SCL L=%d "
-                                          "(loop-faithful C restatement, OpenMP %d threads), %.1f s" % (S, L, th, ct),
-                                   mismatching_frames_vs_gpu=int((ref != got).any(axis=1).sum()))
-        S1 = max(1, S // 16)  # single-core figure (BASELINE.md §3), same frames
-        t0 = time.perf_counter()
-        O.scl_decode(N, L, frozen, llr_h[:S1], threads=1)
-        c1 = time.perf_counter() - t0
-        res["cpu_baseline"]["single_core"] = dict(value=S1 * K / c1 / 1e6, unit="info-Mbps", cores=1,
-                                                  sample="first %d frames, 1 thread, %.1f s" % (S1, c1))
+        res["cpu_baseline"]["c_port"] = dict(
+            value=S2 * K / ct / 1e6, unit="info-Mbps", cores=procs, kind="port",
+            sample="first %d frames, oracle/refcpu.c SCL L=%d (loop-faithful C restatement), OpenMP %d threads, "
+                   "%.1f s" % (S2, L, procs, ct),
+            mismatching_frames_vs_gpu=int((ref != got[:S2]).any(axis=1).sum()))
     return res
 
 
-def bench_ldpc(args, rank, world):
+# ---------------------------------------------------------------- LDPC
+def bench_ldpc(args, rt, pool):
+    from polarcode_and_ldpc_amd import _native
     from polarcode_and_ldpc_amd.channel import AWGNChannel
     from polarcode_and_ldpc_amd.ldpc import BPDecoder, LDPCEncoder
 
@@ -248,88 +326,190 @@ def bench_ldpc(args, rank, world):
     enc = LDPCEncoder(n, k, dv=3, dc=6, seed=42)  # throughput_test.py:285 (rank-251 H, direct solving)
     dec = BPDecoder(enc.H, max_iter=20)
     plan = dec.plan
-    rs = np.random.RandomState(42 + rank)
+    rs = np.random.RandomState(42 + rt.rank)
     U = 4096  # distinct messages, tiled; every frame gets its own noise
     base = enc.encode_batch(rs.randint(0, 2, (U, k)))
     cw = torch.from_numpy(np.tile(base, (B // U + 1, 1))[:B].astype(np.uint8)).cuda()
-    llr = AWGNChannel(args.snr).llr_batch_device(cw, n, B, seed=4242, frame_offset=rank * B)
+    llr = AWGNChannel(args.snr).llr_batch_device(cw, n, B, seed=4242, frame_offset=rt.rank * B)
     out = torch.empty((B, n), dtype=torch.uint8, device="cuda")
     its = torch.empty((B,), dtype=torch.int32, device="cuda")
-    counts = torch.zeros(3, dtype=torch.int64, device="cuda")
-    kt = KernelTimer()
+    dt, per_rank, kms, c = decode_loop(rt, plan, llr, out, cw, k, args.steps, args.warmup, its)
+    kname = {2: "ldpc_reg_kernel<BP,DV=3>", 1: "ldpc_decode_kernel<BP>", 3: "ldpc_check_kernel<BP>"}.get(
+        plan.info.reserved, "?")
+    res = dict(metric="decoded info-Mbps, LDPC (504,252) BP max_iter=20, reference-harness frames @ %.1f dB"
+                      % args.snr,
+               value=B * rt.world * args.steps * k / dt / 1e6, unit="info-Mbps", ms_per_step=dt / args.steps * 1e3,
+               rank_ms_per_step=[t / args.steps * 1e3 for t in per_rank], kernel_ms=kms,
+               mean_iterations=float(its.double().mean().item()),
+               roofline=roofline("ldpc_bp_504", kname, B, 9 * n, kms))
+    res["roofline"]["limit"] = "VALU issue (fp64 transcendentals): see roofline.valu"
+    if not args.skip_extra:
+        # Second frame source (SURVEY §8 d): valid codewords (all-zero; BP is
+        # codeword-symmetric) at the same SNR, early stop on.
+        llr0 = AWGNChannel(args.snr).llr_batch_device(None, n, B, seed=4243, frame_offset=rt.rank * B)
+        out0, its0 = torch.empty_like(out), torch.empty_like(its)
+        dt0, _ = timed_steps(lambda: plan.decode(llr0, out0, its0), args.steps, args.warmup, rt)
+        res["valid_codewords"] = dict(value=B * rt.world * args.steps * k / dt0 / 1e6, unit="info-Mbps",
+                                      ms_per_step=dt0 / args.steps * 1e3,
+                                      mean_iterations=float(its0.double().mean().item()),
+                                      bit_errors=int(out0.sum().item()),
+                                      what="all-zero codeword frames (device AWGN), BP max_iter=20, early stop")
+        del llr0, out0, its0
+    if pool is not None:
+        from oracle import oracle as O
+        from oracle import refnumpy as R
+        from polarcode_and_ldpc_amd.ldpc import dense_to_csr
+        S = args.cpu_frames_numpy
+        llr_h = llr[:max(S, args.cpu_frames_ldpc)].cpu().numpy()
+        got = out[:llr_h.shape[0]].cpu().numpy().astype(np.int64)
+        procs = cpu_processes()
+        res["cpu_baseline"] = numpy_baseline(
+            pool, procs, "BP-20 (504,252)", lambda: R.ldpc_batch(enc.H, llr_h[:S], "bp", 20, True, pool=pool)[0],
+            S, k, got[:S])
+        S2 = args.cpu_frames_ldpc
+        rp, ci = dense_to_csr(enc.H)
+        t0 = time.perf_counter()
+        rb, _ = O.ldpc_decode(rp, ci, n, llr_h[:S2], "bp", 20, True, 1.0, threads=procs)
+        ct = time.perf_counter() - t0
+        res["cpu_baseline"]["c_port"] = dict(
+            value=S2 * k / ct / 1e6, unit="info-Mbps", cores=procs, kind="port",
+            sample="first %d frames, oracle/refcpu.c BP-20, OpenMP %d threads, %.1f s" % (S2, procs, ct),
+            mismatching_frames_vs_gpu=int((rb != got[:S2]).any(axis=1).sum()))
+    return res
 
-    sc = torch.zeros(3, dtype=torch.int64, device="cuda")
+
+# ---------------------------------------------------------------- configs[3], configs[4]
+def bench_cascl(args, rt):
+    """BASELINE configs[3]: CA-SCL N=1024 K=512 L=32 + CRC-8 (the CRC is inside
+    the K info bits, src/polar/encoder.py:74-78)."""
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.harness.ber import simulate_polar
+    from polarcode_and_ldpc_amd.polar import CASCLDecoder, construct_frozen_set
+    from polarcode_and_ldpc_amd.polar.utils import CRC_POLYNOMIALS
+    N, K, L, B = 1024, 512, 32, args.batch
+    fr = construct_frozen_set(N, K, 2.0)
+    dec = CASCLDecoder(N, K, list_size=L, frozen_bits=fr, crc_polynomial="CRC-8")
+    off = rt.rank * B
+    msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    _native.random_bits(44, off, msg)
+    _native.crc_append(msg, K - 8, 8, CRC_POLYNOMIALS["CRC-8"])
+    cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+    _native.polar_encode(dec.plan, msg, cw)
+    llr = AWGNChannel(1.0).llr_batch_device(cw, N, B, seed=44, frame_offset=off)
+    del cw
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    steps = min(args.steps, args.extra_steps)
+    dt, _, kms, c = decode_loop(rt, dec.plan, llr, out, msg, K, steps, 1)
+    res = dict(metric="decoded info-Mbps, CA-SCL N=1024 K=512 L=32 + CRC-8 (BASELINE configs[3]) @ 1.0 dB",
+               value=B * rt.world * steps * K / dt / 1e6, unit="info-Mbps", steps=steps,
+               ms_per_step=dt / steps * 1e3, kernel_ms=kms, frames_per_gpu=B,
+               ber=float(c[0]) / max(1, c[2] * K), fer=float(c[1]) / max(1, c[2]),
+               roofline=roofline("polar_cascl_1024_l32", polar_kernel_name(dec.plan, 10), B, 8 * N + K, kms))
+    del llr, out, msg
+    if not args.skip_sweep:
+        t0 = time.perf_counter()
+        snrs = np.arange(-2.0, 5.5, 1.0)
+        _, _, pts = simulate_polar(snrs, args.sweep_frames, args.sweep_max_errors, {"encoding": {"N": N, "K": K}},
+                                   list_size=L, crc_polynomial="CRC-8", batch=min(B, 32768), seed=3)
+        res["sweep"] = dict(what="harness.ber.simulate_polar: CA-SCL L=32 CRC-8, -2..5 dB Es/N0, max_errors=%d, "
+                                 "<= %d frames per point, frames sharded over %d rank(s), one all-reduce per round"
+                                 % (args.sweep_max_errors, args.sweep_frames, rt.world),
+                            seconds=time.perf_counter() - t0,
+                            points=[dict(snr_db=p.snr_db, frames=p.frames, frame_errors=p.frame_errors,
+                                         bit_errors=p.bit_errors, ber=p.ber, fer=p.fer, fer_ci=list(p.fer_ci))
+                                    for p in pts])
+    return res
+
+
+def bench_long(args, rt):
+    """BASELINE configs[4] per GPU: 1 M frames over 8 GPUs = 131 072 frames each."""
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.ldpc import MSDecoder
+    from polarcode_and_ldpc_amd.ldpc.matrix import regular_construction
+    B = args.long_batch
+    steps = min(args.steps, args.extra_steps)
+    res = {}
+    N, K = 4096, 2048
+    dec, _, msg, llr = polar_fixture(rt, N, K, 8, B, 1.0, 45)
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    dt, _, kms, c = decode_loop(rt, dec.plan, llr, out, msg, K, steps, 1)
+    res["polar_4096_l8"] = dict(
+        metric="decoded info-Mbps, polar N=4096 K=2048 SCL L=8 @ 1.0 dB", value=B * rt.world * steps * K / dt / 1e6,
+        unit="info-Mbps", steps=steps, ms_per_step=dt / steps * 1e3, kernel_ms=kms, frames_per_gpu=B,
+        llr_bytes_per_gpu=B * N * 8, fer=float(c[1]) / max(1, c[2]),
+        roofline=roofline("polar_scl_4096_l8", polar_kernel_name(dec.plan, 12), B, 8 * N + K, kms))
+    del dec, msg, llr, out
+    torch.cuda.empty_cache()
+    n = 8192
+    H = regular_construction(n, 3, 6, seed=11)  # every check degree 6 (min-sum needs >= 2)
+    k = n - H.shape[0]
+    for es in (True, False):
+        dec = MSDecoder(H, max_iter=20, normalization=1.0, early_stop=es)
+        llr = AWGNChannel(1.5).llr_batch_device(None, n, B, seed=46, frame_offset=rt.rank * B)
+        out = torch.empty((B, n), dtype=torch.uint8, device="cuda")
+        its = torch.empty((B,), dtype=torch.int32, device="cuda")
+        zero = torch.zeros((B, k), dtype=torch.uint8, device="cuda")
+        dt, _, kms, c = decode_loop(rt, dec.plan, llr, out, zero, k, steps, 1, its)
+        res["ldpc_8192_ms20" + ("" if es else "_no_early_stop")] = dict(
+            metric="decoded info-Mbps, LDPC n=8192 (3,6)-regular min-sum max_iter=20, all-zero codeword @ 1.5 dB, "
+                   "early stop %s" % ("on" if es else "off"),
+            value=B * rt.world * steps * k / dt / 1e6, unit="info-Mbps", steps=steps, ms_per_step=dt / steps * 1e3,
+            kernel_ms=kms, frames_per_gpu=B, mean_iterations=float(its.double().mean().item()),
+            llr_bytes_per_gpu=B * n * 8, fer=float(c[1]) / max(1, c[2]),
+            roofline=roofline("ldpc_ms_8192" + ("" if es else "_noes"), "ldpc_ms_compact_kernel", B, 9 * n, kms))
+        del llr, out, its, zero, dec
+        torch.cuda.empty_cache()
+    return res
+
+
+# ---------------------------------------------------------------- CPU stub
+def bench_stub(args, rt):
+    """--cpu-stub: the rank / barrier / timing / counter all-reduce path of
+    bench_polar on CPU tensors with a stub decode (hard decision of synthetic
+    LLRs, one bit flipped in every 7th global frame).  A plumbing check: the
+    counters must equal the closed form for the global frame range."""
+    N, K, B = 256, 128, args.batch
+    g = torch.Generator().manual_seed(42 + rt.rank)
+    msg = torch.randint(0, 2, (B, K), generator=g, dtype=torch.uint8)
+    frames = torch.arange(rt.rank * B, (rt.rank + 1) * B)
+    llr = torch.zeros((B, N), dtype=torch.float64)
+    llr[:, :K] = 1.0 - 2.0 * msg.double()
+    flip = frames % 7 == 0
+    llr[flip, (frames[flip] % K)] *= -1.0
+    out = torch.empty_like(msg)
+    counts = torch.zeros(3, dtype=torch.int64)
+    sc = torch.zeros(3, dtype=torch.int64)
 
     def step():
-        kt(lambda: plan.decode(llr, out, its))
-        sc.zero_()
-        _native_count(cw, out, k, sc)
-        if world > 1:
-            dist.all_reduce(sc)
+        out.copy_((llr[:, :K] < 0).to(torch.uint8))
+        e = (out != msg).sum(dim=1)
+        sc.copy_(torch.stack([e.sum(), (e > 0).sum(), torch.tensor(B)]).to(torch.int64))
+        rt.all_reduce(sc)
         counts.add_(sc)
 
-    from polarcode_and_ldpc_amd._native import count_errors as _native_count
-    dt = timed_steps(step, args.steps, args.warmup, world)
-    kt.reset()
-    for _ in range(3):
-        kt(lambda: plan.decode(llr, out, its))
-    kms = kt.mean_ms()
-    value = B * world * args.steps * k / dt / 1e6
-    bpf = 9 * n
-    achieved = B * bpf / (kms / 1e3) / 1e9
-    mean_it = float(its.double().mean().item())
-    res = dict(metric="decoded info-Mbps, LDPC (504,252) BP max_iter=20, reference-harness frames @ %.1f dB" % args.snr,
-               value=value, unit="info-Mbps", ms_per_step=dt / args.steps * 1e3, kernel_ms=kms,
-               mean_iterations=mean_it, vs_published=value / 7.95e-5,
-               roofline=dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
-                             frac=achieved / HBM_PEAK_GBS, traffic=load_traffic("ldpc_bp_504"),
-                             traffic_unit="HBM bytes per launch (2*FETCH_SIZE+WRITE_SIZE, rocprofv3 PMC)",
-                             traffic_source=traffic_source("ldpc_bp_504"),
-                             algorithmic_bytes_per_frame=bpf, frames_per_launch=B, kernel_ms=kms,
-                             kernel={2: "ldpc_reg_kernel<BP,DV=3>", 1: "ldpc_decode_kernel<BP>",
-                                     3: "ldpc_check_kernel<BP>"}.get(plan.info.reserved, "?")))
-    _traffic_rate(res["roofline"])
-    _valu_rate(res["roofline"], "ldpc_bp_504", torch.cuda.get_device_properties(0).multi_processor_count)
-    res["roofline"]["limit"] = "VALU issue (fp64 transcendentals), see roofline.valu; HBM fields are the algorithmic view"
-    if args.skip_extra:
-        return res
-    # Second frame source (SURVEY §8 d): valid codewords (all-zero; BP is
-    # codeword-symmetric) at the same SNR, early stop on.
-    llr0 = AWGNChannel(args.snr).llr_batch_device(None, n, B, seed=4243, frame_offset=rank * B)
-    out0 = torch.empty_like(out)
-    its0 = torch.empty_like(its)
+    dt, per_rank = timed_steps(step, args.steps, args.warmup, rt, on_timed=counts.zero_)
+    return dict(value=B * rt.world * args.steps * K / dt / 1e6, ms_per_step=dt / args.steps * 1e3,
+                rank_ms_per_step=[t / args.steps * 1e3 for t in per_rank],
+                counts=[int(x) for x in counts.tolist()], B=B)
 
-    def step0():
-        plan.decode(llr0, out0, its0)
 
-    dt0 = timed_steps(step0, args.steps, args.warmup, world)
-    res["valid_codewords"] = dict(value=B * world * args.steps * k / dt0 / 1e6, unit="info-Mbps",
-                                  ms_per_step=dt0 / args.steps * 1e3,
-                                  mean_iterations=float(its0.double().mean().item()),
-                                  bit_errors=int(out0.sum().item()),
-                                  what="all-zero codeword frames (device AWGN), BP max_iter=20, early stop")
-    if rank == 0 and world == 1 and not args.skip_cpu:
-        from oracle import oracle as O
-        from polarcode_and_ldpc_amd.ldpc import dense_to_csr
-        S = args.cpu_frames_ldpc
-        th = cpu_threads()
-        rp, ci = dense_to_csr(enc.H)
-        llr_h = llr[:S].cpu().numpy()
-        t0 = time.perf_counter()
-        rb, ri = O.ldpc_decode(rp, ci, n, llr_h, "bp", 20, True, 1.0, threads=th)
-        ct = time.perf_counter() - t0
-        got = out[:S].cpu().numpy().astype(np.int64)
-        res["cpu_baseline"] = dict(value=S * k / ct / 1e6, unit="info-Mbps", cores=th, kind="port",
-                                   sample="first %d frames of the same batch, oracle/refcpu.c BP-20, %d threads, "
-                                          "%.1f s" % (S, th, ct),
-                                   mismatching_frames_vs_gpu=int((rb != got).any(axis=1).sum()))
-        S1 = max(1, S // 16)
-        t0 = time.perf_counter()
-        O.ldpc_decode(rp, ci, n, llr_h[:S1], "bp", 20, True, 1.0, threads=1)
-        c1 = time.perf_counter() - t0
-        res["cpu_baseline"]["single_core"] = dict(value=S1 * k / c1 / 1e6, unit="info-Mbps", cores=1,
-                                                  sample="first %d frames, 1 thread, %.1f s" % (S1, c1))
-    return res
+# ---------------------------------------------------------------- main
+def self_launch(args):
+    """--gpus N > 1 without a torch.distributed environment: start N ranks under
+    torch.distributed.run as a child process (nothing here has touched the GPU)
+    and exit with its status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench.py: launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -340,33 +520,63 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--list-size", type=int, default=8)
     ap.add_argument("--snr", type=float, default=3.0)
-    ap.add_argument("--cpu-frames", type=int, default=8192)
-    ap.add_argument("--cpu-frames-ldpc", type=int, default=65536)
+    ap.add_argument("--cpu-frames", type=int, default=4096, help="frames for the C-port baseline (polar)")
+    ap.add_argument("--cpu-frames-ldpc", type=int, default=32768, help="frames for the C-port baseline (LDPC)")
+    ap.add_argument("--cpu-frames-numpy", type=int, default=256, help="frames for the NumPy baseline")
+    ap.add_argument("--long-batch", type=int, default=131072, help="configs[4] frames per GPU (1 M / 8)")
+    ap.add_argument("--extra-steps", type=int, default=5, help="cap on timed steps of the configs[3]/[4] keys")
+    ap.add_argument("--sweep-frames", type=int, default=131072)
+    ap.add_argument("--sweep-max-errors", type=int, default=200)
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--skip-ldpc", action="store_true")
+    ap.add_argument("--skip-configs", action="store_true", help="no configs[3]/[4] keys")
+    ap.add_argument("--skip-sweep", action="store_true", help="no CA-SCL BER sweep")
     ap.add_argument("--skip-extra", action="store_true",
-                    help="only the headline decodes (no end-to-end / valid-codeword runs): profiling passes")
+                    help="only the headline decodes (no end-to-end / valid-codeword / configs[3,4] runs): profiling")
+    ap.add_argument("--cpu-stub", action="store_true", help="CPU/gloo plumbing check with a stub decode")
     args = ap.parse_args()
+    if args.skip_extra:
+        args.skip_configs = True
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args))
 
-    pol = bench_polar(args, rank, world)
-    ldp = None if args.skip_ldpc else bench_ldpc(args, rank, world)
-    if rank == 0:
+    rt = Runtime(args.cpu_stub)
+    if args.cpu_stub:
+        r = bench_stub(args, rt)
+        if rt.rank == 0:
+            print(json.dumps({"metric": METRIC + " [cpu-stub plumbing check, not a measurement]", "value": r["value"],
+                              "unit": "info-Mbps", "n_gpus": rt.world, "steps": args.steps, "warmup": args.warmup,
+                              "ms_per_step": r["ms_per_step"], "rank_ms_per_step": r["rank_ms_per_step"],
+                              "higher_is_better": True, "scaling": "weak", "stub": True, "counts": r["counts"],
+                              "frames_per_rank": r["B"]}), flush=True)
+        rt.close()
+        return
+
+    # the CPU-baseline pool is spawned before the first GPU call (rank 0, N = 1)
+    pool = None
+    if rt.rank == 0 and rt.world == 1 and not args.skip_cpu:
+        from oracle import refnumpy as R
+        pool = R.make_pool(cpu_processes())
+    pol = bench_polar(args, rt, pool)
+    ldp = None if args.skip_ldpc else bench_ldpc(args, rt, pool)
+    if pool is not None:
+        pool.close()
+    extra = {}
+    if not args.skip_configs:
+        extra["cascl_l32"] = bench_cascl(args, rt)
+        extra["long_block"] = bench_long(args, rt)
+    if rt.rank == 0:
         line = {
-            "metric": METRIC, "value": pol["value"], "unit": "info-Mbps", "n_gpus": world,
+            "metric": METRIC, "value": pol["value"], "unit": "info-Mbps", "n_gpus": rt.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": pol["ms_per_step"],
+            "rank_ms_per_step": pol["rank_ms_per_step"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: random messages, device polar encoder, device AWGN (Philox) at %.1f dB Es/N0" % args.snr,
-            "config": {"workload": "polar N=1024 K=512 SCL L=%d decode, bit-reversed Bhattacharyya(2 dB) frozen set"
-                                   % args.list_size,
-                       "global_batch": args.batch * world, "frames_per_gpu": args.batch,
-                       "parallelism": "frame-sharded x%d (one RCCL all-reduce of error counters per step)" % world},
+            "config": {"workload": "polar N=1024 K=512 SCL L=%d decode (BASELINE configs[1]), bit-reversed "
+                                   "Bhattacharyya(2 dB) frozen set" % args.list_size,
+                       "global_batch": args.batch * rt.world, "frames_per_gpu": args.batch,
+                       "parallelism": "frame-sharded x%d (one RCCL all-reduce of error counters per step)" % rt.world},
             "roofline": pol["roofline"],
             "cpu_baseline": pol.get("cpu_baseline"),
             "ber": pol["ber"], "fer": pol["fer"], "plan": pol["plan"],
@@ -374,9 +584,9 @@ def main():
         }
         if ldp is not None:
             line["ldpc"] = ldp
+        line.update(extra)
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    rt.close()
 
 
 if __name__ == "__main__":

@@ -41,7 +41,7 @@ typedef struct {
     int32_t lds_bytes;  /* dynamic LDS per workgroup of the decode kernel          */
     int32_t fused_top;  /* polar: tree depths fused into the channel read (>=1)    */
     int32_t frames_per_block; /* frames one workgroup decodes                     */
-    int32_t reserved;   /* polar: kernel generation (4 tree, 3 lane, 1 group);     
+    int32_t reserved;   /* polar: kernel generation (4 tree, 3 lane);
                            LDPC: 2 register-cached, 1 generic, 3 thread-per-check,
                            5 min-sum with compressed check state */
 } pl_plan_info;
@@ -55,8 +55,10 @@ typedef struct {
  *   (the reference's 0 < K < N assertion, decoder.py:17-18, is made by the
  *   Python layer on its K argument, exactly as the reference does).
  *   flags: 0 = fastest kernel built for (N, list size).  Diagnostics: bits 0-3
- *   force the lane kernel (polar_lane.hip) with that fused-top depth, 0x10 the
- *   group kernel, 0x20 the lane kernel with its default depth. */
+ *   force the lane kernel (polar_lane.hip) with that fused-top depth, 0x10 or
+ *   0x20 the lane kernel with its default depth.
+ *   The plan owns device constants only; decode workspace is per stream (grown
+ *   lazily to the batch, see pl_decode) or caller-supplied (pl_decode_ws). */
 int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_mask, int32_t list_size,
                          int32_t flags, pl_plan** out);
 
@@ -83,17 +85,35 @@ int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr, const int3
  *   SCLDecoder.decode (:225-262), BPDecoder.decode (src/ldpc/decoder.py:124-202)
  *   and MSDecoder.decode (:289-352) applied to `batch` frames.
  *   llr_dev : fp64 [batch][ld] device, row b = channel LLRs of frame b (n_in used)
- *   bits_dev: uint8 [batch][n_out] device.  Polar: u_hat[info_bits] ascending;
- *             LDPC: the full hard-decision word (decoded = total <= 0).
+ *   bits_dev: uint8 [batch][n_out] device, rows contiguous (pitch n_out).
+ *             Polar: u_hat[info_bits] ascending; LDPC: the full hard-decision
+ *             word (decoded = total <= 0).
  *   iters_dev: int32 [batch] device or NULL; LDPC: iterations run (BPDecoder's
  *             return_iterations); polar: ignored.
- *   Asynchronous on `stream`.  Deterministic (no atomics in the decode path). */
+ *   Asynchronous on `stream`.  Deterministic (no atomics in the decode path).
+ *   Workspace: the plan keeps one device buffer per stream, sized on first use
+ *   to this batch (polar: one slice per resident wavefront, at most the
+ *   persistent grid; LDPC codes whose messages exceed LDS: one per frame of a
+ *   chunk) and grown when a larger batch arrives (after draining that stream).
+ *   Host threads may share a plan when each uses its own stream; calls on one
+ *   stream are serialised by the plan. */
 int pl_decode(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
               int32_t* iters_dev, void* stream);
 
-/* Pre-allocate the plan's device workspace for up to max_batch frames, so that
- * pl_decode never allocates (needed before hipGraph capture of pl_decode). */
-int pl_plan_reserve(pl_plan* plan, int64_t max_batch);
+/* Workspace bytes pl_decode_ws needs to decode `batch` frames at full speed
+ * (0: the kernel needs none).  Any size >= one unit works: a smaller
+ * workspace runs fewer resident wavefronts / smaller LDPC chunks. */
+int pl_plan_workspace_bytes(const pl_plan* plan, int64_t batch, int64_t* bytes);
+
+/* pl_decode with a caller-supplied device workspace (the caller owns it and
+ * must not use it concurrently elsewhere); no allocation, so safe inside
+ * hipGraph capture. */
+int pl_decode_ws(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
+                 int32_t* iters_dev, void* workspace_dev, int64_t workspace_bytes, void* stream);
+
+/* Pre-allocate `stream`'s workspace for batches up to max_batch, so that
+ * pl_decode on that stream never allocates. */
+int pl_plan_reserve(pl_plan* plan, int64_t max_batch, void* stream);
 
 int pl_plan_get_info(const pl_plan* plan, pl_plan_info* info);
 int pl_plan_destroy(pl_plan* plan);
@@ -103,9 +123,8 @@ const char* pl_last_error(void);
  * per-phase s_memtime cycle totals (summed over all frames) into stamps_dev[8]:
  * tree kernel (pl_plan_info.reserved == 4): [0] fused top, [1] workspace chains,
  * [2] LDS chain, [3] path metrics, [4] pruning/cloning, [5] partial-sum walk,
- * [6] final selection/output, [7] workspace fences; group kernel: [0] LLR update,
- * [1] metrics, [2] pruning, [3] walk, [4] final.  Timing differs from pl_decode;
- * read shares. */
+ * [6] final selection/output, [7] workspace fences.  Timing differs from
+ * pl_decode; read shares. */
 int pl_debug_polar_stamps(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
                           unsigned long long* stamps_dev, void* stream);
 

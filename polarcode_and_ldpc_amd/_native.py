@@ -23,7 +23,7 @@ EXPORTS = (
     "pl_polar_plan_create", "pl_ldpc_plan_create", "pl_decode", "pl_plan_reserve", "pl_plan_get_info",
     "pl_plan_destroy", "pl_last_error", "pl_random_bits", "pl_polar_encode", "pl_awgn_llr",
     "pl_count_errors", "pl_debug_polar_stamps", "pl_polar_plan_set_crc", "pl_crc_append",
-    "pl_rayleigh_llr", "pl_bsc", "pl_gf2_encode",
+    "pl_rayleigh_llr", "pl_bsc", "pl_gf2_encode", "pl_decode_ws", "pl_plan_workspace_bytes",
 )
 
 
@@ -45,7 +45,9 @@ def _load():
     L.pl_polar_plan_create.argtypes = [I32, I32, P, I32, I32, PP]
     L.pl_ldpc_plan_create.argtypes = [I32, I32, P, P, I32, I32, I32, D, I32, PP]
     L.pl_decode.argtypes = [P, P, I64, I64, P, P, P]
-    L.pl_plan_reserve.argtypes = [P, I64]
+    L.pl_plan_reserve.argtypes = [P, I64, P]
+    L.pl_decode_ws.argtypes = [P, P, I64, I64, P, P, P, I64, P]
+    L.pl_plan_workspace_bytes.argtypes = [P, I64, ctypes.POINTER(ctypes.c_int64)]
     L.pl_plan_get_info.argtypes = [P, ctypes.POINTER(PlanInfo)]
     L.pl_plan_destroy.argtypes = [P]
     L.pl_last_error.restype = ctypes.c_char_p
@@ -105,7 +107,8 @@ def require_gpu():
 
 
 class Plan:
-    """Owner of a pl_plan*; immutable after creation."""
+    """Owner of a pl_plan*.  The plan holds device constants; decode workspace is
+    per stream (grown lazily by the library) or caller-supplied (decode(ws=...))."""
 
     def __init__(self, handle: ctypes.c_void_p):
         self._h = handle
@@ -117,17 +120,42 @@ class Plan:
     def handle(self):
         return self._h
 
-    def reserve(self, max_batch: int):
-        check(lib.pl_plan_reserve(self._h, int(max_batch)), "pl_plan_reserve")
+    def reserve(self, max_batch: int, stream=None):
+        """Pre-size `stream`'s workspace (default: torch's current stream)."""
+        check(lib.pl_plan_reserve(self._h, int(max_batch), ctypes.c_void_p(_stream(stream))), "pl_plan_reserve")
 
-    def decode(self, llr: "torch.Tensor", bits: "torch.Tensor", iters: "torch.Tensor | None" = None, stream=None):
-        """llr fp64 [B, >=n_in] (contiguous rows), bits uint8 [B, n_out], iters int32 [B] or None."""
-        assert llr.dtype == torch.float64 and llr.dim() == 2 and llr.stride(1) == 1
-        assert bits.dtype == torch.uint8 and bits.shape == (llr.shape[0], self.info.n_out)
+    def workspace_bytes(self, batch: int) -> int:
+        b = ctypes.c_int64()
+        check(lib.pl_plan_workspace_bytes(self._h, int(batch), ctypes.byref(b)), "pl_plan_workspace_bytes")
+        return int(b.value)
+
+    def _check(self, llr, bits, iters):
+        # the kernels write bits at row pitch n_out and iters densely; llr rows
+        # may carry any pitch >= n_in but unit inner stride (ADVICE r1)
+        assert isinstance(llr, torch.Tensor) and llr.is_cuda, "llr must be a device tensor"
+        assert llr.dtype == torch.float64 and llr.dim() == 2 and llr.stride(1) == 1 and llr.shape[1] >= self.info.n_in
+        assert bits.is_cuda and bits.dtype == torch.uint8 and bits.shape == (llr.shape[0], self.info.n_out)
+        assert bits.is_contiguous(), "bits must be contiguous [B, n_out] (row pitch n_out)"
+        if iters is not None:
+            assert iters.is_cuda and iters.dtype == torch.int32 and iters.shape == (llr.shape[0],) \
+                and iters.is_contiguous(), "iters must be a contiguous int32 [B] device tensor"
+
+    def decode(self, llr: "torch.Tensor", bits: "torch.Tensor", iters: "torch.Tensor | None" = None, stream=None,
+               ws: "torch.Tensor | None" = None):
+        """llr fp64 [B, >=n_in] device, bits uint8 [B, n_out] contiguous, iters int32 [B]
+        or None; ws: optional caller-owned uint8 device workspace (pl_decode_ws)."""
+        self._check(llr, bits, iters)
         B = llr.shape[0]
-        it = _dptr(iters) if iters is not None else None
-        check(lib.pl_decode(self._h, ctypes.c_void_p(llr.data_ptr()), B, _ld(llr), _dptr(bits), it,
-                            ctypes.c_void_p(_stream(stream))), "pl_decode")
+        it = ctypes.c_void_p(iters.data_ptr()) if iters is not None else None
+        st = ctypes.c_void_p(_stream(stream))
+        if ws is None:
+            check(lib.pl_decode(self._h, ctypes.c_void_p(llr.data_ptr()), B, _ld(llr),
+                                ctypes.c_void_p(bits.data_ptr()), it, st), "pl_decode")
+        else:
+            assert ws.is_cuda and ws.is_contiguous()
+            check(lib.pl_decode_ws(self._h, ctypes.c_void_p(llr.data_ptr()), B, _ld(llr),
+                                   ctypes.c_void_p(bits.data_ptr()), it, ctypes.c_void_p(ws.data_ptr()),
+                                   ws.numel() * ws.element_size(), st), "pl_decode_ws")
 
     def decode_stamped(self, llr: "torch.Tensor", bits: "torch.Tensor", stamps: "torch.Tensor", stream=None):
         """Diagnostic decode accumulating per-phase cycle totals into stamps (int64 [5])."""

@@ -8,16 +8,25 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "internal.hpp"
+
+// Device workspace of one stream (polar: per resident wavefront; LDPC codes
+// whose messages exceed LDS: per frame of a chunk).  Grown lazily to the batch.
+struct Workspace {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
 
 struct pl_plan {
     int kind = 0;  // 0 polar, 1 ldpc
     int device = 0;
     // polar
-    pl::PolarGeom pg{};
+    pl::PolarGeom pg{};  // N, K, F, lds_bytes of the chosen kernel
     bool sc = false;
     int list_size = 0;
     uint32_t* d_frozen_dec = nullptr;  // decode-order frozen bitmask [ceil(N/32)]
@@ -25,21 +34,29 @@ struct pl_plan {
     int32_t* d_pos2info = nullptr;     // [N] index -> info rank or -1
     uint32_t* d_crc_g = nullptr;       // CA-SCL: CRC contribution of x_hat bit j [N] (null = plain SCL)
     std::vector<int32_t> h_info;       // ascending info positions (host copy)
-    bool tree = false;      // v4 compile-time-geometry kernel (polar_tree.hip)
+    bool tree = false;      // compile-time-geometry kernel (polar_tree.hip); else polar_lane.hip
     pl::TreeInfo tinfo{};
-    bool lane = false;      // lane-per-path kernel (polar_lane.hip)
     pl::LaneGeom lgeo{};
+    int fpw = 1;            // frames per wavefront
     int lane_grid_max = 0;  // resident wavefronts (persistent grid)
-    unsigned char* lane_ws = nullptr;
     // ldpc
     pl::LdpcGeom lg{};
     pl::LdpcDev ld{};
     int32_t* d_ldpc = nullptr;
-    double* work = nullptr;
-    int64_t work_frames = 0;
+    int64_t ldpc_chunk = 16384;  // frames per launch of the global-workspace kernel
+    // workspace: bytes per unit (polar: one resident wave; LDPC global: one
+    // frame), one buffer per stream (plans are shared across host threads that
+    // use distinct streams; a decode only ever touches its stream's buffer)
+    size_t ws_unit = 0;
+    std::mutex mu;
+    std::unordered_map<hipStream_t, Workspace> ws;
 };
 
 static thread_local std::string g_err;
+
+// HIP caps a launch at 2^32 work-items per grid dimension; per-frame kernels
+// (one workgroup per frame) are launched in chunks below 2^31 work-items.
+constexpr int64_t kMaxLaunchItems = 1LL << 31;
 
 static int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -72,6 +89,13 @@ static int env_int(const char* name, int dflt) {
     return (s && *s) ? std::atoi(s) : dflt;
 }
 
+static int device_cus(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+        return prop.multiProcessorCount;
+    return 256;
+}
+
 extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_mask, int32_t list_size,
                                     int32_t flags, pl_plan** out) {
     if (!out) return fail(PL_EINVAL, "out is NULL");
@@ -99,106 +123,43 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
     p->list_size = list_size;
     hipGetDevice(&p->device);
     const char* kern = std::getenv("PL_POLAR_KERNEL");
-    const std::string kname = kern ? kern : "";
-    {
-        int lcap = 1;
-        while (lcap < (p->sc ? 1 : list_size)) lcap <<= 1;
-        p->tree = kname != "lane" && kname != "group" && !(flags & 0x3F) &&
-                  pl::tree_lookup(n, lcap, p->sc, &p->tinfo);
-    }
-    if (p->tree) {
-        hipError_t e;
-        p->pg.N = N; p->pg.K = K; p->pg.F = p->tinfo.F; p->pg.lds_bytes = p->tinfo.lds_bytes;
-        if ((e = upload(&p->d_frozen_dec, fdec)) != hipSuccess || (e = upload(&p->d_info_pos, info)) != hipSuccess ||
-            (e = upload(&p->d_pos2info, pos2info)) != hipSuccess) {
-            pl_plan_destroy(p);
-            return hipfail(e, "plan upload");
-        }
-        int per_cu = 1;
-        if ((e = pl::tree_prepare(p->tinfo, &per_cu)) != hipSuccess) {
-            pl_plan_destroy(p);
-            return hipfail(e, "tree kernel prepare");
-        }
-        hipDeviceProp_t prop;
-        int cus = 256;
-        if (hipGetDeviceProperties(&prop, p->device) == hipSuccess && prop.multiProcessorCount > 0)
-            cus = prop.multiProcessorCount;
-        p->lane_grid_max = per_cu * cus;
-        const int waves_env = env_int("PL_POLAR_WAVES", 0);
-        if (waves_env > 0) p->lane_grid_max = waves_env;
-        if ((e = hipMalloc((void**)&p->lane_ws, (size_t)p->tinfo.ws_bytes * p->lane_grid_max)) != hipSuccess) {
-            pl_plan_destroy(p);
-            return hipfail(e, "tree workspace");
-        }
-        *out = p;
-        return PL_OK;
-    }
-    p->lane = kname != "group" && !(flags & 0x10);
-    if (p->lane) {
-        int F = flags & 0xF;
-        if (!F) F = env_int("PL_POLAR_FUSED", 3);
-        const int budget = env_int("PL_POLAR_LDS_BUDGET", 8 * 1024);
-        pl::lane_geom(N, K, p->sc ? 1 : list_size, F, budget, &p->lgeo);
-        p->pg.N = N; p->pg.K = K; p->pg.F = p->lgeo.F; p->pg.lds_bytes = p->lgeo.lds_bytes;
-        hipError_t e;
-        if ((e = upload(&p->d_frozen_dec, fdec)) != hipSuccess || (e = upload(&p->d_info_pos, info)) != hipSuccess ||
-            (e = upload(&p->d_pos2info, pos2info)) != hipSuccess) {
-            pl_plan_destroy(p);
-            return hipfail(e, "plan upload");
-        }
-        int per_cu = 1;
-        if ((e = pl::lane_prepare(p->lgeo, p->sc, &per_cu)) != hipSuccess) {
-            pl_plan_destroy(p);
-            return hipfail(e, "lane kernel prepare");
-        }
-        hipDeviceProp_t prop;
-        int cus = 256;
-        if (hipGetDeviceProperties(&prop, p->device) == hipSuccess && prop.multiProcessorCount > 0)
-            cus = prop.multiProcessorCount;
-        p->lane_grid_max = per_cu * cus;
-        const int waves_env = env_int("PL_POLAR_WAVES", 0);
-        if (waves_env > 0) p->lane_grid_max = waves_env;
-        if ((e = hipMalloc((void**)&p->lane_ws, (size_t)p->lgeo.ws_bytes * p->lane_grid_max)) != hipSuccess) {
-            pl_plan_destroy(p);
-            return hipfail(e, "lane workspace");
-        }
-        *out = p;
-        return PL_OK;
-    }
-    // fused-top depth: flags bits 0..3 (or env PL_POLAR_FUSED) override; else the
-    // smallest F whose LDS footprint fits the occupancy budget.
-    int F = flags & 0xF;
-    if (!F) F = env_int("PL_POLAR_FUSED", 0);
-    const int budget = env_int("PL_POLAR_LDS_BUDGET", 48 * 1024);
-    const int Lgeom = p->sc ? 1 : list_size;
-    if (!F) {
-        F = 0;
-        for (int f = 1; f <= 4 && f <= n; ++f) {
-            pl::PolarGeom g;
-            if (pl::polar_geom(N, K, Lgeom, f, &g) <= budget) { F = f; break; }
-        }
-        if (!F) {
-            for (int f = 1; f <= 4 && f <= n; ++f) {
-                pl::PolarGeom g;
-                if (pl::polar_geom(N, K, Lgeom, f, &g) <= 160 * 1024) { F = f; break; }
-            }
-        }
-        if (!F) { delete p; return fail(PL_EUNSUPPORTED, "decoder state exceeds LDS (N/list too large)"); }
-    }
-    if (F > 4) F = 4;
-    pl::polar_geom(N, K, Lgeom, F, &p->pg);
-    if (p->pg.lds_bytes > 160 * 1024) { delete p; return fail(PL_EUNSUPPORTED, "decoder state exceeds LDS"); }
+    int lcap = 1;
+    while (lcap < (p->sc ? 1 : list_size)) lcap <<= 1;
+    p->tree = !(kern && std::string(kern) == "lane") && !(flags & 0x3F) && pl::tree_lookup(n, lcap, p->sc, &p->tinfo);
     hipError_t e;
-    if ((e = upload(&p->d_frozen_dec, fdec)) != hipSuccess ||
-        (e = upload(&p->d_info_pos, info)) != hipSuccess ||
+    if ((e = upload(&p->d_frozen_dec, fdec)) != hipSuccess || (e = upload(&p->d_info_pos, info)) != hipSuccess ||
         (e = upload(&p->d_pos2info, pos2info)) != hipSuccess) {
         pl_plan_destroy(p);
         return hipfail(e, "plan upload");
     }
-    if ((e = pl::polar_prepare(p->pg, p->sc)) != hipSuccess) {
-        pl_plan_destroy(p);
-        return hipfail(e, "hipFuncSetAttribute");
+    p->pg.N = N;
+    p->pg.K = K;
+    int per_cu = 1;
+    if (p->tree) {
+        p->pg.F = p->tinfo.F;
+        p->pg.lds_bytes = p->tinfo.lds_bytes;
+        p->fpw = p->tinfo.fpw;
+        p->ws_unit = (size_t)p->tinfo.ws_bytes;
+        e = pl::tree_prepare(p->tinfo, &per_cu);
+    } else {
+        // lane-per-path kernel for every (N, L) without a tree instance; flags
+        // bits 0..3 pick its fused-top depth (diagnostic), 0x10 / 0x20 force it
+        int F = flags & 0xF;
+        if (!F) F = env_int("PL_POLAR_FUSED", 3);
+        pl::lane_geom(N, K, p->sc ? 1 : list_size, F, env_int("PL_POLAR_LDS_BUDGET", 8 * 1024), &p->lgeo);
+        p->pg.F = p->lgeo.F;
+        p->pg.lds_bytes = p->lgeo.lds_bytes;
+        p->fpw = 64 / p->lgeo.lcap;
+        p->ws_unit = (size_t)p->lgeo.ws_bytes;
+        e = pl::lane_prepare(p->lgeo, p->sc, &per_cu);
     }
+    if (e != hipSuccess) {
+        pl_plan_destroy(p);
+        return hipfail(e, "polar kernel prepare");
+    }
+    p->lane_grid_max = per_cu * device_cus(p->device);
+    const int waves_env = env_int("PL_POLAR_WAVES", 0);
+    if (waves_env > 0) p->lane_grid_max = waves_env;
     *out = p;
     return PL_OK;
 }
@@ -332,96 +293,150 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     p->ld.var_chk = p->ld.edge_meta + E;
     p->ld.var_cp = p->ld.var_chk + E;
     if ((e = pl::ldpc_prepare(g)) != hipSuccess) { pl_plan_destroy(p); return hipfail(e, "hipFuncSetAttribute"); }
+    p->ws_unit = pl::ldpc_work_bytes_per_frame(g);
+    p->ldpc_chunk = std::max(1, env_int("PL_LDPC_CHUNK", 16384));
     *out = p;
     return PL_OK;
 }
 
-static int reserve(pl_plan* p, int64_t frames) {
-    if (p->kind != 1 || !p->lg.use_global || frames <= p->work_frames) return PL_OK;
-    if (p->work) { hipFree(p->work); p->work = nullptr; p->work_frames = 0; }
-    const size_t bytes = pl::ldpc_work_bytes_per_frame(p->lg) * (size_t)frames;
-    hipError_t e = hipMalloc((void**)&p->work, bytes);
-    if (e != hipSuccess) return hipfail(e, "workspace");
-    p->work_frames = frames;
-    return PL_OK;
-}
-
-extern "C" int pl_plan_reserve(pl_plan* p, int64_t max_batch) {
-    if (!p) return fail(PL_EINVAL, "plan is NULL");
-    const int64_t chunk = env_int("PL_LDPC_CHUNK", 16384);
-    return reserve(p, max_batch < chunk ? max_batch : chunk);
-}
-
-extern "C" int pl_decode(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
-                         int32_t* iters, void* stream) {
-    if (!p) return fail(PL_EINVAL, "plan is NULL");
-    if (batch < 0) return fail(PL_EINVAL, "batch < 0");
-    if (batch == 0) return PL_OK;
-    if (!llr || !bits) return fail(PL_EINVAL, "NULL buffer");
-    hipStream_t s = (hipStream_t)stream;
+// Workspace bytes a decode of `batch` frames uses at full speed.
+static size_t ws_need(const pl_plan* p, int64_t batch) {
+    if (batch <= 0 || p->ws_unit == 0) return 0;
     if (p->kind == 0) {
-        if (ld < p->pg.N) return fail(PL_EINVAL, "ld < N");
-        if (p->tree) {
-            const int64_t need = (batch + p->tinfo.fpw - 1) / p->tinfo.fpw;
-            const int grid = (int)(need < p->lane_grid_max ? need : p->lane_grid_max);
-            hipError_t e = pl::tree_launch(p->tinfo, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, p->pg.K,
-                                           p->sc ? 1 : p->list_size, p->lane_ws, grid, nullptr, p->d_crc_g, s);
-            return e == hipSuccess ? PL_OK : hipfail(e, "polar decode launch");
+        const int64_t waves = (batch + p->fpw - 1) / p->fpw;
+        return p->ws_unit * (size_t)std::min<int64_t>(waves, p->lane_grid_max);
+    }
+    return p->ws_unit * (size_t)std::min<int64_t>(batch, p->ldpc_chunk);
+}
+
+// Decode with an explicit workspace of ws_bytes (>= one unit when one is needed):
+// the polar grid / LDPC chunk is clamped to what the workspace holds.
+static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits, int32_t* iters,
+                       void* ws, size_t ws_bytes, unsigned long long* stamps, hipStream_t s) {
+    if (p->ws_unit > 0 && (ws == nullptr || ws_bytes < p->ws_unit))
+        return fail(PL_EINVAL, "workspace smaller than one unit (pl_plan_workspace_bytes)");
+    if (p->kind == 0) {
+        const int64_t waves = (batch + p->fpw - 1) / p->fpw;
+        const int64_t fit = (int64_t)(ws_bytes / p->ws_unit);
+        const int grid = (int)std::min<int64_t>(std::min<int64_t>(waves, p->lane_grid_max), fit);
+        hipError_t e;
+        if (p->tree)
+            e = pl::tree_launch(p->tinfo, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, p->pg.K,
+                                p->sc ? 1 : p->list_size, (unsigned char*)ws, grid, stamps, p->d_crc_g, s);
+        else if (stamps)
+            return fail(PL_EUNSUPPORTED, "stamps only for the tree kernel");
+        else
+            e = pl::lane_launch(p->lgeo, p->sc, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch,
+                                (unsigned char*)ws, grid, p->d_crc_g, s);
+        return e == hipSuccess ? PL_OK : hipfail(e, "polar decode launch");
+    }
+    if (!p->lg.use_global) {
+        // one workgroup per frame; HIP caps a grid at 2^32 work-items
+        const int64_t step = kMaxLaunchItems / p->lg.threads;
+        for (int64_t b0 = 0; b0 < batch; b0 += step) {
+            const int64_t nb = std::min<int64_t>(step, batch - b0);
+            hipError_t e = pl::ldpc_launch(p->lg, p->ld, llr + b0 * ld, ld, bits + b0 * p->lg.n,
+                                           iters ? iters + b0 : nullptr, nb, nullptr, s);
+            if (e != hipSuccess) return hipfail(e, "ldpc decode launch");
         }
-        if (p->lane) {
-            const int fpw = 64 / p->lgeo.lcap;
-            const int64_t need = (batch + fpw - 1) / fpw;
-            const int grid = (int)(need < p->lane_grid_max ? need : p->lane_grid_max);
-            hipError_t e = pl::lane_launch(p->lgeo, p->sc, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch,
-                                           p->lane_ws, grid, p->d_crc_g, s);
-            return e == hipSuccess ? PL_OK : hipfail(e, "polar decode launch");
-        }
-        hipError_t e = pl::polar_launch(p->pg, p->sc, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, s);
-        if (e != hipSuccess) return hipfail(e, "polar decode launch");
         return PL_OK;
     }
-    if (ld < p->lg.n) return fail(PL_EINVAL, "ld < n");
-    if (!p->lg.use_global) {
-        hipError_t e = pl::ldpc_launch(p->lg, p->ld, llr, ld, bits, iters, batch, nullptr, s);
-        return e == hipSuccess ? PL_OK : hipfail(e, "ldpc decode launch");
-    }
-    const int64_t chunk = env_int("PL_LDPC_CHUNK", 16384);
-    int rc = reserve(p, batch < chunk ? batch : chunk);
-    if (rc) return rc;
-    for (int64_t b0 = 0; b0 < batch; b0 += p->work_frames) {
-        const int64_t nb = std::min<int64_t>(p->work_frames, batch - b0);
+    const int64_t chunk = std::min<int64_t>(p->ldpc_chunk, (int64_t)(ws_bytes / p->ws_unit));
+    for (int64_t b0 = 0; b0 < batch; b0 += chunk) {
+        const int64_t nb = std::min<int64_t>(chunk, batch - b0);
         hipError_t e = pl::ldpc_launch(p->lg, p->ld, llr + b0 * ld, ld, bits + b0 * p->lg.n,
-                                       iters ? iters + b0 : nullptr, nb, p->work, s);
+                                       iters ? iters + b0 : nullptr, nb, (double*)ws, s);
         if (e != hipSuccess) return hipfail(e, "ldpc decode launch");
     }
     return PL_OK;
 }
 
+// The calling stream's workspace, grown to `need` bytes.  A buffer is only
+// ever used by its own stream, so before it is replaced only that stream has
+// to drain.  Caller holds p->mu.
+static int stream_ws(pl_plan* p, hipStream_t s, size_t need, Workspace** out) {
+    Workspace& w = p->ws[s];
+    if (w.bytes < need) {
+        if (w.ptr) {
+            hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return hipfail(e, "workspace regrow: stream synchronize");
+            hipFree(w.ptr);
+            w.ptr = nullptr;
+            w.bytes = 0;
+        }
+        hipError_t e = hipMalloc(&w.ptr, need);
+        if (e != hipSuccess) {
+            w.ptr = nullptr;
+            return hipfail(e, "decode workspace");
+        }
+        w.bytes = need;
+    }
+    *out = &w;
+    return PL_OK;
+}
+
+static int check_decode_args(const pl_plan* p, int64_t batch, int64_t ld, const void* llr, const void* bits) {
+    if (!p) return fail(PL_EINVAL, "plan is NULL");
+    if (batch < 0) return fail(PL_EINVAL, "batch < 0");
+    if (batch > 0 && (!llr || !bits)) return fail(PL_EINVAL, "NULL buffer");
+    if (p->kind == 0 && ld < p->pg.N) return fail(PL_EINVAL, "ld < N");
+    if (p->kind == 1 && ld < p->lg.n) return fail(PL_EINVAL, "ld < n");
+    return PL_OK;
+}
+
+extern "C" int pl_plan_reserve(pl_plan* p, int64_t max_batch, void* stream) {
+    if (!p) return fail(PL_EINVAL, "plan is NULL");
+    const size_t need = ws_need(p, max_batch);
+    if (need == 0) return PL_OK;
+    std::lock_guard<std::mutex> lk(p->mu);
+    Workspace* w;
+    return stream_ws(p, (hipStream_t)stream, need, &w);
+}
+
+extern "C" int pl_plan_workspace_bytes(const pl_plan* p, int64_t batch, int64_t* bytes) {
+    if (!p || !bytes) return fail(PL_EINVAL, "NULL argument");
+    if (batch < 0) return fail(PL_EINVAL, "batch < 0");
+    *bytes = (int64_t)ws_need(p, batch);
+    return PL_OK;
+}
+
+extern "C" int pl_decode(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
+                         int32_t* iters, void* stream) {
+    int rc = check_decode_args(p, batch, ld, llr, bits);
+    if (rc || batch == 0) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(p->mu);
+    const size_t need = ws_need(p, batch);
+    Workspace* w = nullptr;
+    if (need && (rc = stream_ws(p, s, need, &w))) return rc;
+    return decode_impl(p, llr, batch, ld, bits, iters, w ? w->ptr : nullptr, w ? w->bytes : 0, nullptr, s);
+}
+
+extern "C" int pl_decode_ws(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
+                            int32_t* iters, void* workspace, int64_t workspace_bytes, void* stream) {
+    int rc = check_decode_args(p, batch, ld, llr, bits);
+    if (rc || batch == 0) return rc;
+    if (workspace_bytes < 0) return fail(PL_EINVAL, "workspace_bytes < 0");
+    return decode_impl(p, llr, batch, ld, bits, iters, workspace, (size_t)workspace_bytes, nullptr,
+                       (hipStream_t)stream);
+}
+
 extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
                                      unsigned long long* stamps_dev, void* stream) {
     if (!p || p->kind != 0 || !stamps_dev) return fail(PL_EINVAL, "polar plan and stamp buffer required");
-    if (p->tree) {
-        if (ld < p->pg.N) return fail(PL_EINVAL, "ld < N");
-        if (batch <= 0) return PL_OK;
-        const int64_t need = (batch + p->tinfo.fpw - 1) / p->tinfo.fpw;
-        const int grid = (int)(need < p->lane_grid_max ? need : p->lane_grid_max);
-        hipError_t e = pl::tree_launch(p->tinfo, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, p->pg.K,
-                                       p->sc ? 1 : p->list_size, p->lane_ws, grid, stamps_dev, p->d_crc_g,
-                                       (hipStream_t)stream);
-        return e == hipSuccess ? PL_OK : hipfail(e, "polar stamps launch");
-    }
-    if (p->lane) return fail(PL_EUNSUPPORTED, "stamps only for the tree and group kernels");
-    if (!p->sc && p->pg.lcap != 8) return fail(PL_EUNSUPPORTED, "stamps build only for SC and list size 5..8");
-    hipError_t e = pl::polar_launch(p->pg, p->sc, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch,
-                                    (hipStream_t)stream, stamps_dev);
-    return e == hipSuccess ? PL_OK : hipfail(e, "polar stamps launch");
+    int rc = check_decode_args(p, batch, ld, llr, bits);
+    if (rc || batch == 0) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(p->mu);
+    Workspace* w = nullptr;
+    if ((rc = stream_ws(p, s, ws_need(p, batch), &w))) return rc;
+    return decode_impl(p, llr, batch, ld, bits, nullptr, w->ptr, w->bytes, stamps_dev, s);
 }
 
 extern "C" int pl_polar_plan_set_crc(pl_plan* p, int32_t crc_len, uint32_t poly) {
     if (!p || p->kind != 0) return fail(PL_EINVAL, "not a polar plan");
     if (p->sc) return fail(PL_EINVAL, "CRC-aided selection needs a list decoder (list_size >= 1)");
     if (crc_len < 0 || crc_len > 32) return fail(PL_EINVAL, "crc_len must be in [0, 32]");
-    if (!p->tree && !p->lane) return fail(PL_EUNSUPPORTED, "CRC-aided selection not built for the group kernel");
     if (p->d_crc_g) { hipFree(p->d_crc_g); p->d_crc_g = nullptr; }
     if (crc_len == 0) return PL_OK;
     const int N = p->pg.N;
@@ -449,8 +464,8 @@ extern "C" int pl_plan_get_info(const pl_plan* p, pl_plan_info* info) {
     if (p->kind == 0) {
         info->kind = 0; info->n_in = p->pg.N; info->n_out = p->pg.K; info->list_size = p->list_size;
         info->lds_bytes = p->pg.lds_bytes; info->fused_top = p->pg.F;
-        info->frames_per_block = p->tree ? p->tinfo.fpw : (p->lane ? 64 / p->lgeo.lcap : 1);
-        info->reserved = p->tree ? 4 : (p->lane ? 3 : 1);  // kernel generation: 4 tree, 3 lane, 1 group
+        info->frames_per_block = p->fpw;
+        info->reserved = p->tree ? 4 : 3;  // kernel generation: 4 tree, 3 lane
     } else {
         info->kind = 1; info->n_in = p->lg.n; info->n_out = p->lg.n; info->list_size = 0;
         info->lds_bytes = p->lg.lds_bytes; info->fused_top = 0; info->frames_per_block = 1;
@@ -468,8 +483,8 @@ extern "C" int pl_plan_destroy(pl_plan* p) {
     if (p->d_pos2info) hipFree(p->d_pos2info);
     if (p->d_crc_g) hipFree(p->d_crc_g);
     if (p->d_ldpc) hipFree(p->d_ldpc);
-    if (p->work) hipFree(p->work);
-    if (p->lane_ws) hipFree(p->lane_ws);
+    for (auto& kv : p->ws)
+        if (kv.second.ptr) hipFree(kv.second.ptr);  // hipFree waits for work that still uses it
     delete p;
     return PL_OK;
 }
@@ -484,8 +499,14 @@ extern "C" int pl_random_bits(uint64_t seed, int64_t frame_offset, int64_t batch
 extern "C" int pl_polar_encode(const pl_plan* p, const uint8_t* msg, int64_t batch, uint8_t* cw, void* stream) {
     if (!p || p->kind != 0) return fail(PL_EINVAL, "not a polar plan");
     if (batch < 0 || (batch > 0 && (!msg || !cw))) return fail(PL_EINVAL, "bad argument");
-    hipError_t e = pl::polar_encode_launch(p->pg.N, p->pg.K, p->d_pos2info, msg, batch, cw, (hipStream_t)stream);
-    return e == hipSuccess ? PL_OK : hipfail(e, "polar encode launch");
+    const int64_t step = kMaxLaunchItems / 64;  // one wavefront per frame
+    for (int64_t b0 = 0; b0 < batch; b0 += step) {
+        const int64_t nb = std::min<int64_t>(step, batch - b0);
+        hipError_t e = pl::polar_encode_launch(p->pg.N, p->pg.K, p->d_pos2info, msg + b0 * p->pg.K, nb,
+                                               cw + b0 * p->pg.N, (hipStream_t)stream);
+        if (e != hipSuccess) return hipfail(e, "polar encode launch");
+    }
+    return PL_OK;
 }
 
 extern "C" int pl_awgn_llr(const uint8_t* cw, int32_t n, int64_t batch, double snr_db, uint64_t seed,
@@ -530,8 +551,14 @@ extern "C" int pl_gf2_encode(const uint32_t* g_dev, int32_t k, int32_t n, const 
                              int64_t batch, uint8_t* cw, int64_t ld_cw, void* stream) {
     if (batch < 0 || k < 1 || n < 1 || ld_msg < k || ld_cw < n || (batch > 0 && (!g_dev || !msg || !cw)))
         return fail(PL_EINVAL, "bad argument");
-    hipError_t e = pl::gf2_encode_launch(g_dev, k, n, msg, ld_msg, batch, cw, ld_cw, (hipStream_t)stream);
-    return e == hipSuccess ? PL_OK : hipfail(e, "gf2 encode launch");
+    const int64_t step = kMaxLaunchItems / 64;  // one wavefront per frame
+    for (int64_t b0 = 0; b0 < batch; b0 += step) {
+        const int64_t nb = std::min<int64_t>(step, batch - b0);
+        hipError_t e = pl::gf2_encode_launch(g_dev, k, n, msg + b0 * ld_msg, ld_msg, nb, cw + b0 * ld_cw, ld_cw,
+                                             (hipStream_t)stream);
+        if (e != hipSuccess) return hipfail(e, "gf2 encode launch");
+    }
+    return PL_OK;
 }
 
 extern "C" int pl_count_errors(const uint8_t* ref, int64_t ldr, const uint8_t* dec, int64_t ldd, int32_t width,

@@ -10,10 +10,12 @@
 
 namespace pl {
 
-// one thread per 32 message bits
-__global__ void random_bits_kernel(uint64_t seed, int64_t off, int64_t batch, int k, uint8_t* bits) {
+// one thread per 32 message bits; rows whose 32-bit groups are 16-byte aligned
+// (vec) are written as two 16-byte stores of 0/1 bytes instead of 32 byte stores
+__global__ void random_bits_kernel(uint64_t seed, int64_t off, int64_t batch, int k, uint8_t* bits, int vec,
+                                   int64_t base) {
     const int wpf = (k + 31) / 32;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t idx = base + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= batch * wpf) return;
     const int64_t b = idx / wpf;
     const int w = (int)(idx % wpf);
@@ -23,6 +25,18 @@ __global__ void random_bits_kernel(uint64_t seed, int64_t off, int64_t batch, in
     const uint32_t x = r.x;
     uint8_t* o = bits + b * k + w * 32;
     const int cnt = (k - w * 32) < 32 ? (k - w * 32) : 32;
+    if (vec && cnt == 32) {
+        uint32_t q[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const uint32_t nib = (x >> (4 * t)) & 0xFu;  // bytes 4t..4t+3 = bits 4t..4t+3
+            q[t] = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
+        }
+        uint4* o4 = reinterpret_cast<uint4*>(o);
+        o4[0] = make_uint4(q[0], q[1], q[2], q[3]);
+        o4[1] = make_uint4(q[4], q[5], q[6], q[7]);
+        return;
+    }
     for (int j = 0; j < cnt; ++j) o[j] = (x >> j) & 1u;
 }
 
@@ -96,11 +110,14 @@ gf2_encode_kernel(const uint32_t* __restrict__ g, int k, int n, const uint8_t* _
     }
 }
 
-// two LLRs per thread (one Philox call -> two 53-bit uniforms -> Box-Muller pair)
+// two LLRs per thread (one Philox call -> two 53-bit uniforms -> Box-Muller
+// pair); with even n and ld and aligned rows (vec) one 2-byte codeword load and
+// one 16-byte LLR store per thread
 __global__ void awgn_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch, double sigma,
-                            double sigma2, uint64_t seed, int64_t off, double* __restrict__ llr, int64_t ld) {
+                            double sigma2, uint64_t seed, int64_t off, double* __restrict__ llr, int64_t ld,
+                            int vec, int64_t base) {
     const int ppf = (n + 1) / 2;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t idx = base + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= batch * ppf) return;
     const int64_t b = idx / ppf;
     const int q = (int)(idx % ppf);
@@ -115,6 +132,17 @@ __global__ void awgn_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch
     sincospi(2.0 * u2, &sn, &cs);
     const double z[2] = {rad * cs, rad * sn};
     double* o = llr + b * ld;
+    if (vec) {
+        double s0 = 1.0, s1 = 1.0;
+        if (cw) {
+            const uint16_t pr = *reinterpret_cast<const uint16_t*>(cw + b * n + 2 * q);
+            s0 = 1.0 - 2.0 * (double)(pr & 1u);
+            s1 = 1.0 - 2.0 * (double)((pr >> 8) & 1u);
+        }
+        const double y0 = s0 + sigma * z[0], y1 = s1 + sigma * z[1];  // awgn.py:47, :88
+        reinterpret_cast<double2*>(o)[q] = make_double2(2.0 * y0 / sigma2, 2.0 * y1 / sigma2);  // awgn.py:75
+        return;
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int j = 2 * q + h;
@@ -143,8 +171,8 @@ PL_DEV void normal_pair(uint64_t seed, uint32_t salt, uint32_t ctr, uint64_t f, 
 // h_r, h_i ~ N(0, 1/2); y = h s + N(0, sigma); LLR = 2 y h / sigma^2 (CSI at the
 // receiver).  One thread per bit, Philox keyed by (seed, global frame, bit).
 __global__ void rayleigh_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch, double sigma, double sigma2,
-                                uint64_t seed, int64_t off, double* __restrict__ llr, int64_t ld) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                uint64_t seed, int64_t off, double* __restrict__ llr, int64_t ld, int64_t base) {
+    const int64_t idx = base + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= batch * n) return;
     const int64_t b = idx / n;
     const int j = (int)(idx % n);
@@ -161,8 +189,8 @@ __global__ void rayleigh_kernel(const uint8_t* __restrict__ cw, int n, int64_t b
 // Binary symmetric channel (src/channel/bsc.py:33-49): out = bit ^ (u < p),
 // u uniform in [0, 1) per bit.
 __global__ void bsc_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch, double p, uint64_t seed,
-                           int64_t off, uint8_t* __restrict__ out, int64_t ld) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                           int64_t off, uint8_t* __restrict__ out, int64_t ld, int64_t base) {
+    const int64_t idx = base + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= batch * n) return;
     const int64_t b = idx / n;
     const int j = (int)(idx % n);
@@ -174,22 +202,34 @@ __global__ void bsc_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch,
     out[b * ld + j] = bit ^ (uint8_t)(u < p ? 1 : 0);
 }
 
+// HIP caps a launch at 2^32 work-items per grid dimension: element-wise
+// launches over more work-items (1 M frames x 8192 bits) go in chunks of 2^30.
+constexpr int64_t kChunkItems = 1LL << 30;
+
+template <typename Launch>
+static hipError_t chunked(int64_t tot, Launch&& launch) {
+    for (int64_t base = 0; base < tot; base += kChunkItems) {
+        const int64_t items = tot - base < kChunkItems ? tot - base : kChunkItems;
+        launch(dim3((unsigned)((items + 255) / 256)), base);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t rayleigh_launch(const uint8_t* cw, int n, int64_t batch, double sigma, double sigma2, uint64_t seed,
                            int64_t off, double* llr, int64_t ld, hipStream_t s) {
-    const int64_t tot = batch * n;
-    if (tot == 0) return hipSuccess;
-    hipLaunchKernelGGL(rayleigh_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, cw, n, batch, sigma,
-                       sigma2, seed, off, llr, ld);
-    return hipGetLastError();
+    return chunked(batch * n, [&](dim3 grid, int64_t base) {
+        hipLaunchKernelGGL(rayleigh_kernel, grid, dim3(256), 0, s, cw, n, batch, sigma, sigma2, seed, off, llr, ld,
+                           base);
+    });
 }
 
 hipError_t bsc_launch(const uint8_t* cw, int n, int64_t batch, double p, uint64_t seed, int64_t off, uint8_t* out,
                       int64_t ld, hipStream_t s) {
-    const int64_t tot = batch * n;
-    if (tot == 0) return hipSuccess;
-    hipLaunchKernelGGL(bsc_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, cw, n, batch, p, seed, off,
-                       out, ld);
-    return hipGetLastError();
+    return chunked(batch * n, [&](dim3 grid, int64_t base) {
+        hipLaunchKernelGGL(bsc_kernel, grid, dim3(256), 0, s, cw, n, batch, p, seed, off, out, ld, base);
+    });
 }
 
 // one wavefront per frame; per-block partial sums -> 3 integer atomics
@@ -220,11 +260,10 @@ count_errors_kernel(const uint8_t* __restrict__ ref, int64_t ldr, const uint8_t*
 
 hipError_t random_bits_launch(uint64_t seed, int64_t off, int64_t batch, int k, uint8_t* bits,
                               hipStream_t s) {
-    const int64_t tot = batch * ((k + 31) / 32);
-    if (tot == 0) return hipSuccess;
-    hipLaunchKernelGGL(random_bits_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seed, off,
-                       batch, k, bits);
-    return hipGetLastError();
+    const int vec = (k % 16 == 0) && (((uintptr_t)bits & 15) == 0);
+    return chunked(batch * ((k + 31) / 32), [&](dim3 grid, int64_t base) {
+        hipLaunchKernelGGL(random_bits_kernel, grid, dim3(256), 0, s, seed, off, batch, k, bits, vec, base);
+    });
 }
 
 hipError_t polar_encode_launch(int N, int K, const int32_t* pos2info, const uint8_t* msg, int64_t batch,
@@ -247,11 +286,11 @@ hipError_t gf2_encode_launch(const uint32_t* g, int k, int n, const uint8_t* msg
 
 hipError_t awgn_launch(const uint8_t* cw, int n, int64_t batch, double sigma, double sigma2, uint64_t seed,
                        int64_t off, double* llr, int64_t ld, hipStream_t s) {
-    const int64_t tot = batch * ((n + 1) / 2);
-    if (tot == 0) return hipSuccess;
-    hipLaunchKernelGGL(awgn_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, cw, n, batch, sigma,
-                       sigma2, seed, off, llr, ld);
-    return hipGetLastError();
+    const int vec = (n % 2 == 0) && (ld % 2 == 0) && (((uintptr_t)llr & 15) == 0) && (((uintptr_t)cw & 1) == 0);
+    return chunked(batch * ((n + 1) / 2), [&](dim3 grid, int64_t base) {
+        hipLaunchKernelGGL(awgn_kernel, grid, dim3(256), 0, s, cw, n, batch, sigma, sigma2, seed, off, llr, ld, vec,
+                           base);
+    });
 }
 
 // CRC append (src/polar/utils.py:86-125 crc_encode, bit-serial MSB first, zero

@@ -7,17 +7,10 @@ namespace pl {
 
 constexpr int kMaxDepth = 15;  // N <= 2^15
 
-// LDS layout of one frame's list-decoder state (one wave = one frame).
+// What pl_plan_get_info reports about a polar plan's kernel.
 struct PolarGeom {
-    int N, n, K, Lsz, F, lcap;
+    int N, K, F;
     int lds_bytes;
-    int cw;                    // words of the transform / walk scratch (max(1, N/32))
-    int llr_off[kMaxDepth + 2];  // byte offset of the LLR pool at depth d (F <= d < n)
-    int bl_off[kMaxDepth + 2];   // byte offset of the left-beta pool at depth d (1 <= d <= n)
-    int bl_words[kMaxDepth + 2]; // u32 words per slot at depth d
-    int cur_off;               // [lcap][2][cw] u32 ping-pong walk scratch
-    int tab_off;               // [lcap][32] bytes: LLR slot ptr [0..15], beta slot ptr [16..31]
-    int surv_off;              // [lcap] x 16 B survivor table
 };
 
 // Lane-per-path decoder (polar_lane.hip): one lane = one list path, 64/lcap
@@ -54,12 +47,6 @@ hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t
                        const int32_t* info_pos, int64_t batch, int K, int Lsz, unsigned char* ws, int grid,
                        unsigned long long* stamps, const uint32_t* crc_g, hipStream_t s);
 
-int polar_lcap(int list_size);  // lane-group count (power of two) for a list size
-int polar_geom(int N, int K, int list_size, int F, PolarGeom* g);  // fills layout, returns lds bytes
-hipError_t polar_launch(const PolarGeom& g, bool sc, const double* llr, int64_t ld, uint8_t* out,
-                        const uint32_t* frozen_dec, const int32_t* info_pos, int64_t batch,
-                        hipStream_t s, unsigned long long* stamps = nullptr);
-hipError_t polar_prepare(const PolarGeom& g, bool sc);  // raise the kernel's LDS limit
 
 hipError_t polar_encode_launch(int N, int K, const int32_t* pos2info, const uint8_t* msg,
                                int64_t batch, uint8_t* cw, hipStream_t s);

@@ -23,14 +23,21 @@ from typing import Dict, Optional, Sequence
 import numpy as np
 
 from ..utils.visualization import save_results
-from .montecarlo import MonteCarlo, ldpc_round_fn, polar_round_fn
+from .montecarlo import MonteCarlo, PointLog, ldpc_round_fn, polar_round_fn
+
+
+def _log(log_path, mc, **key):
+    if not log_path:
+        return None
+    return PointLog(log_path, dict(key, round_frames=mc.batch * mc.world))
 
 
 def simulate_polar(snr_db_range: Sequence[float], num_frames: int, max_errors: int, config: Dict,
                    list_size: int = 0, crc_polynomial: Optional[str] = None, batch: int = 65536, seed: int = 0,
-                   group=None):
+                   group=None, log_path=None):
     """ber_simulation.py:132-198 -> (ber, fer, points).  list_size 0 = SC (the
-    reference), >= 1 = SCL, with crc_polynomial = CA-SCL (CRC inside the K bits)."""
+    reference), >= 1 = SCL, with crc_polynomial = CA-SCL (CRC inside the K bits).
+    log_path: JSON-lines file of finished points; a rerun resumes from it."""
     import torch
     from ..lib_wrappers import PolarLibWrapper
     from ..polar.decoder import CASCLDecoder, SCDecoder, SCLDecoder
@@ -44,12 +51,14 @@ def simulate_polar(snr_db_range: Sequence[float], num_frames: int, max_errors: i
         dec = SCLDecoder(N, K, list_size, frozen_bits=fr)
     mc = MonteCarlo(polar_round_fn(dec, seed=seed, crc_polynomial=crc_polynomial), info_bits=K, batch=batch,
                     group=group, device=torch.device("cuda", torch.cuda.current_device()))
-    pts = mc.run(snr_db_range, num_frames, max_errors)
+    log = _log(log_path, mc, code="polar", N=N, K=K, list_size=list_size, crc=crc_polynomial, frames=num_frames,
+               max_errors=max_errors, seed=seed)
+    pts = mc.run(snr_db_range, num_frames, max_errors, log=log)
     return np.array([p.ber for p in pts]), np.array([p.fer for p in pts]), pts
 
 
 def simulate_ldpc(snr_db_range: Sequence[float], num_frames: int, max_errors: int, config: Dict,
-                  batch: int = 65536, seed: int = 0, group=None, random_codewords: bool = False):
+                  batch: int = 65536, seed: int = 0, group=None, random_codewords: bool = False, log_path=None):
     """ber_simulation.py:201-293 -> (ber, fer, points).  random_codewords: random
     messages encoded into valid codewords on the device (LDPCEncoder.
     encode_batch_device) instead of the all-zero codeword."""
@@ -65,7 +74,9 @@ def simulate_ldpc(snr_db_range: Sequence[float], num_frames: int, max_errors: in
     enc = LDPCEncoder(n, lib.k, H=H) if random_codewords else None
     mc = MonteCarlo(ldpc_round_fn(dec, seed=seed, info_bits=lib.k, encoder=enc), info_bits=lib.k, batch=batch,
                     group=group, device=torch.device("cuda", torch.cuda.current_device()))
-    pts = mc.run(snr_db_range, num_frames, max_errors)
+    log = _log(log_path, mc, code="ldpc", n=n, k=lib.k, max_iter=dec.max_iter, random=random_codewords,
+               frames=num_frames, max_errors=max_errors, seed=seed)
+    pts = mc.run(snr_db_range, num_frames, max_errors, log=log)
     return np.array([p.ber for p in pts]), np.array([p.fer for p in pts]), pts
 
 
@@ -74,9 +85,11 @@ def run_ber_simulation(snr_db_range: np.ndarray, num_frames: int, max_errors: in
                        list_size: int = 0, crc_polynomial: Optional[str] = None) -> Dict:
     snr = np.asarray(snr_db_range, dtype=float)
     results = {"snr_db": snr.tolist(), "polar": {}, "ldpc": {}}
-    pb, pf, pp = simulate_polar(snr, num_frames, max_errors, polar_config, list_size, crc_polynomial, batch)
+    points = Path(output_dir) / "data" / "ber_points.jsonl"  # per-point rows: an interrupted run resumes
+    pb, pf, pp = simulate_polar(snr, num_frames, max_errors, polar_config, list_size, crc_polynomial, batch,
+                                log_path=points)
     results["polar"]["self"] = {"ber": pb.tolist(), "fer": pf.tolist(), "points": [p.as_dict() for p in pp]}
-    lb, lf, lp = simulate_ldpc(snr, num_frames, max_errors, ldpc_config, batch)
+    lb, lf, lp = simulate_ldpc(snr, num_frames, max_errors, ldpc_config, batch, log_path=points)
     results["ldpc"]["self"] = {"ber": lb.tolist(), "fer": lf.tolist(), "points": [p.as_dict() for p in lp]}
     if use_third_party:
         print("Warning: third-party libraries (polarcodes, pyldpc) are not available offline")
@@ -112,6 +125,7 @@ def main(argv=None):
     ap.add_argument("--max-errors", type=int, default=100)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--log", default=None, help="JSON-lines file of finished SNR points; a rerun resumes from it")
     ap.add_argument("--ldpc-codewords", choices=["zero", "random"], default="zero",
                     help="LDPC frames: all-zero codeword, or random messages encoded on the device")
     a = ap.parse_args(argv)
@@ -123,11 +137,11 @@ def main(argv=None):
     snr = _parse_range(a.snr)
     if a.code == "polar":
         ber, fer, pts = simulate_polar(snr, a.frames, a.max_errors, {"encoding": {"N": a.N, "K": a.K}},
-                                       a.list_size, a.crc, a.batch)
+                                       a.list_size, a.crc, a.batch, log_path=a.log)
     else:
         ber, fer, pts = simulate_ldpc(snr, a.frames, a.max_errors,
                                       {"encoding": {"n": a.n, "k": a.k}, "decoding": {"max_iterations": a.max_iter}},
-                                      a.batch, random_codewords=a.ldpc_codewords == "random")
+                                      a.batch, random_codewords=a.ldpc_codewords == "random", log_path=a.log)
     if int(os.environ.get("RANK", "0")) == 0:
         res = {"code": a.code, "snr_db": snr.tolist(), "ber": ber.tolist(), "fer": fer.tolist(), "gpus": world,
                "points": [p.as_dict() for p in pts]}

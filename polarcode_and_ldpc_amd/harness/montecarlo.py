@@ -110,8 +110,78 @@ class MonteCarlo:
             done += round_total
         return res.finalize()
 
-    def run(self, snr_db_range: Sequence[float], num_frames: int, max_errors: int) -> List[PointResult]:
-        return [self.run_point(i, s, num_frames, max_errors) for i, s in enumerate(snr_db_range)]
+    def run(self, snr_db_range: Sequence[float], num_frames: int, max_errors: int,
+            log: "Optional[PointLog]" = None) -> List[PointResult]:
+        """One PointResult per SNR point.  With a PointLog, points already in the
+        log (same run key) are taken from it, and each new point is appended as
+        soon as it finishes (rank 0), so an interrupted sweep resumes where it
+        stopped.  Point i always draws the stream (seed, i, frame): a resumed
+        sweep gives the same counts as an uninterrupted one."""
+        done = log.load() if log is not None else {}
+        out = []
+        for i, s in enumerate(snr_db_range):
+            key = round(float(s), 9)
+            if key in done:
+                out.append(done[key])
+                continue
+            p = self.run_point(i, s, num_frames, max_errors)
+            if log is not None and self.rank == 0:
+                log.append(p)
+            out.append(p)
+        return out
+
+
+class PointLog:
+    """Append-only JSON-lines record of finished SNR points (SURVEY §5
+    checkpoint / resume; the reference writes its results once at the end,
+    src/utils/visualization.py:84-112).  Each row carries the run key (code,
+    decoder, frames, max_errors, frames per round, seed): rows of another
+    configuration in the same file are ignored."""
+
+    def __init__(self, path, key: dict):
+        import json
+        import os
+        self.path = str(path)
+        self.key = json.loads(json.dumps(key, sort_keys=True))
+        d = os.path.dirname(self.path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+
+    def load(self):
+        import json
+        import os
+        done = {}
+        if not os.path.exists(self.path):
+            return done
+        with open(self.path) as f:
+            for line in f:
+                line = line.strip()
+                if not line:
+                    continue
+                try:
+                    row = json.loads(line)
+                except ValueError:
+                    continue  # a row cut short by an interruption
+                if row.get("key") != self.key:
+                    continue
+                p = row["point"]
+                r = PointResult(snr_db=p["snr_db"], frames=p["frames"], frame_errors=p["frame_errors"],
+                                bit_errors=p["bit_errors"], info_bits=p["info_bits"], rounds=p.get("rounds", 0))
+                done[round(float(r.snr_db), 9)] = r.finalize()
+        return done
+
+    def append(self, p: PointResult):
+        import json
+        import os
+        with open(self.path, "ab+") as f:
+            f.seek(0, os.SEEK_END)
+            if f.tell() > 0:  # a torn last row (interrupted write) keeps its own line
+                f.seek(-1, os.SEEK_END)
+                if f.read(1) != b"\n":
+                    f.write(b"\n")
+            f.write((json.dumps({"key": self.key, "point": p.as_dict()}) + "\n").encode())
+            f.flush()
+            os.fsync(f.fileno())
 
 
 # ---------------------------------------------------------------------------

@@ -3,7 +3,7 @@
 Same constructors, attributes and `.decode(llr)` contract as the reference's
 src/polar/decoder.py (SCDecoder :12-173, SCLDecoder :176-444); adds
 `decode_batch` (host or device arrays) for batched decoding.  All decoding runs
-in libpolarldpc.so (polar_list.hip); there is no CPU path.
+in libpolarldpc.so (polar_tree.hip / polar_lane.hip); there is no CPU path.
 """
 from __future__ import annotations
 

@@ -187,6 +187,35 @@ def job_scl4096_l8():
     return job_scl(4096, 2048, 8, (1.5,), 3, 10, "polar_scl_4096_l8.npz")
 
 
+# Round 2: wider reference-held parity where last-ulp metric differences could
+# flip a near-tie rank -- low SNR (config 4's sweep starts at -2 dB), large
+# lists and long codes near the waterfall.  One job per SNR point so the pool
+# runs them in parallel (the reference takes ~2.4 s per L=32 frame, ~8 s per
+# N=4096 L=8 frame).
+def _job_scl_l32_low(var, snr, seed):
+    def job():
+        name = "polar_scl_1024_l32_m%d.npz" % int(round(-snr * 10))
+        return job_scl(1024, 512, 32, (snr,), 64, seed, name)
+    job.__name__ = job.__qualname__ = var  # picklable by module attribute
+    return job
+
+
+def _job_scl4096_wf(var, snr, seed):
+    def job():
+        name = "polar_scl_4096_l8_wf%d.npz" % int(round(-snr * 10))
+        return job_scl(4096, 2048, 8, (snr,), 8, seed, name)
+    job.__name__ = job.__qualname__ = var
+    return job
+
+
+job_scl1024_l32_m20 = _job_scl_l32_low("job_scl1024_l32_m20", -2.0, 201)
+job_scl1024_l32_m10 = _job_scl_l32_low("job_scl1024_l32_m10", -1.0, 202)
+job_scl1024_l32_m00 = _job_scl_l32_low("job_scl1024_l32_m00", 0.0, 203)
+job_scl4096_wf_a = _job_scl4096_wf("job_scl4096_wf_a", -1.5, 211)
+job_scl4096_wf_b = _job_scl4096_wf("job_scl4096_wf_b", -1.0, 212)
+ROUND2_JOBS = [job_scl1024_l32_m20, job_scl1024_l32_m10, job_scl1024_l32_m00, job_scl4096_wf_a, job_scl4096_wf_b]
+
+
 def job_small():
     """Small N, odd list sizes, K extremes, zero LLRs (deterministic cases)."""
     polar, _, channel = _imp()
@@ -426,7 +455,8 @@ def job_polar_erasures():
 
 
 JOBS = [job_scl4096_l8, job_scl1024_l8, job_ms8192, job_scl1024_l32, job_bp504,
-        job_sc1024, job_ms504, job_small, job_p1, job_kat16, job_crc, job_ldpc_special, job_polar_erasures]
+        job_sc1024, job_ms504, job_small, job_p1, job_kat16, job_crc, job_ldpc_special, job_polar_erasures
+        ] + ROUND2_JOBS
 
 
 def _run(fn):

@@ -1,0 +1,154 @@
+"""BER/FER parity of the device Monte-Carlo chain with the reference's CPU path
+(BASELINE.json north_star: "BER/FER curves agree within Monte-Carlo error at
+every SNR point"), and the distribution of the device AWGN source.
+
+Device side (the product path): harness.montecarlo -- device random messages
+(Philox), device polar encoder or the all-zero LDPC codeword, pl_awgn_llr
+(Philox4x32-10 + Box-Muller), the HIP decoder, device error count.
+
+Reference side: the frame loop of benchmarks/ber_simulation.py:167-192 --
+np.random.randint messages, the host encoder (equal to the reference's,
+tests/test_host.py), the reference channel (AWGNChannel.transmit: np.random.normal,
+src/channel/awgn.py:75, :88), decoded by the C oracle (bit-exact with the
+reference decoders, tests/test_oracle_golden.py).
+
+Criteria (fixed seeds, so the outcome is deterministic):
+  * FER: the 95 % Wilson intervals of src/utils/metrics.py:138-167 overlap;
+  * BER: bit errors within a frame are correlated (a wrong frame carries many),
+    so a Wilson interval over bits is far too narrow; the BER check is a
+    two-sample z-test on bit errors per frame (frames are the independent
+    units), |z| < 3.5.  The 95 % bit-level Wilson intervals are reported.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _host_polar(oracle, N, K, L, fr, snr, frames, seed, chunk=2048):
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.polar import PolarEncoder
+    enc = PolarEncoder(N, K, frozen_bits=fr)
+    np.random.seed(seed)
+    ch = AWGNChannel(snr)
+    per_frame = []
+    for c0 in range(0, frames, chunk):
+        m = np.random.randint(0, 2, (min(chunk, frames - c0), K))
+        llr = ch.transmit(enc.encode_batch(m), return_llr=True)
+        dec = oracle.sc_decode(N, fr, llr, threads=16) if L == 0 else oracle.scl_decode(N, L, fr, llr, threads=16)
+        per_frame.append((dec != m).sum(axis=1))
+    return np.concatenate(per_frame)
+
+
+def _host_ldpc(oracle, H, k, snr, frames, seed, max_iter=20):
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.ldpc import dense_to_csr
+    np.random.seed(seed)
+    ch = AWGNChannel(snr)
+    n = H.shape[1]
+    llr = ch.transmit(np.zeros((frames, n), dtype=int), return_llr=True)
+    rp, ci = dense_to_csr(H)
+    bits, _ = oracle.ldpc_decode(rp, ci, n, llr, "bp", max_iter, True, 1.0, threads=16)
+    return bits[:, :k].sum(axis=1)
+
+
+def _compare(dev, host_err, K, label):
+    from polarcode_and_ldpc_amd.harness.montecarlo import wilson_interval
+    nh = len(host_err)
+    fh, bh = int((host_err > 0).sum()), int(host_err.sum())
+    _, lo_d, hi_d = wilson_interval(dev.frame_errors, dev.frames)
+    _, lo_h, hi_h = wilson_interval(fh, nh)
+    assert lo_d <= hi_h and lo_h <= hi_d, "%s FER: device %.4g [%.4g, %.4g] vs reference %.4g [%.4g, %.4g]" % (
+        label, dev.fer, lo_d, hi_d, fh / nh, lo_h, hi_h)
+    # BER: per-frame bit-error counts are the independent units
+    var = float(np.var(host_err, ddof=1)) if nh > 1 else 0.0
+    md, mh = dev.bit_errors / dev.frames, bh / nh
+    se = math.sqrt(var / dev.frames + var / nh)
+    z = 0.0 if se == 0 else (md - mh) / se
+    assert abs(z) < 3.5, "%s BER: device %.4g vs reference %.4g (z = %.2f)" % (label, md / K, mh / K, z)
+    return dict(fer_dev=dev.fer, fer_ref=fh / nh, ber_dev=md / K, ber_ref=mh / K, z=z)
+
+
+@pytest.mark.parametrize("snr", [-2.0, -1.0, 0.0])
+def test_sc_n256_ber_fer_parity(gpu, oracle, snr):
+    from polarcode_and_ldpc_amd.harness.montecarlo import MonteCarlo, polar_round_fn
+    from polarcode_and_ldpc_amd.polar import SCDecoder, construct_frozen_set
+    N, K = 256, 128
+    fr = construct_frozen_set(N, K, 2.0)  # ber_simulation.py:146-148 (PolarLibWrapper substitute)
+    dev = MonteCarlo(polar_round_fn(SCDecoder(N, K, frozen_bits=fr), seed=101), info_bits=K,
+                     batch=65536).run([snr], 131072, 10 ** 12)[0]
+    host = _host_polar(oracle, N, K, 0, fr, snr, 20000, seed=int(1000 + 10 * snr))
+    r = _compare(dev, host, K, "SC N=256 @ %g dB" % snr)
+    assert r["fer_ref"] > 0.005  # a point with errors to compare
+
+
+@pytest.mark.parametrize("snr", [-2.0, -1.5, -1.0])
+def test_scl_l8_n1024_ber_fer_parity(gpu, oracle, snr):
+    """SCL L=8 N=1024 in its waterfall (Es/N0, the reference's SNR: FER ~6 % at
+    -1.5 dB; at 0 / 1 dB FER is below 1e-3 and both sides see ~0 errors in a
+    test-sized sample)."""
+    from polarcode_and_ldpc_amd.harness.montecarlo import MonteCarlo, polar_round_fn
+    from polarcode_and_ldpc_amd.polar import SCLDecoder, construct_frozen_set
+    N, K, L = 1024, 512, 8
+    fr = construct_frozen_set(N, K, 2.0)
+    dev = MonteCarlo(polar_round_fn(SCLDecoder(N, K, L, frozen_bits=fr), seed=102), info_bits=K,
+                     batch=65536).run([snr], 131072, 10 ** 12)[0]
+    host = _host_polar(oracle, N, K, L, fr, snr, 2048, seed=int(2000 + 10 * snr))
+    _compare(dev, host, K, "SCL L=8 N=1024 @ %g dB" % snr)
+
+
+@pytest.mark.parametrize("snr", [-1.0, 0.5])
+def test_bp20_504_ber_fer_parity(gpu, oracle, snr):
+    """BP-20 on the seed-42 (504, 252) code, all-zero codeword (BP is
+    codeword-symmetric; the device side is harness.montecarlo.ldpc_round_fn),
+    errors over the first k positions as ber_simulation.py:265-269."""
+    from polarcode_and_ldpc_amd.harness.montecarlo import MonteCarlo, ldpc_round_fn
+    from polarcode_and_ldpc_amd.ldpc import BPDecoder, LDPCEncoder
+    enc = LDPCEncoder(504, 252, dv=3, dc=6, seed=42)
+    dec = BPDecoder(enc.H, max_iter=20)
+    dev = MonteCarlo(ldpc_round_fn(dec, seed=103, info_bits=252), info_bits=252,
+                     batch=65536).run([snr], 131072, 10 ** 12)[0]
+    host = _host_ldpc(oracle, np.asarray(enc.H), 252, snr, 20000, seed=int(3000 + 10 * snr))
+    r = _compare(dev, host, 252, "BP-20 (504,252) @ %g dB" % snr)
+    assert r["fer_ref"] > 0.001
+
+
+def test_awgn_llr_moments_and_tails(gpu):
+    """pl_awgn_llr against the reference channel's distribution: for the all-zero
+    codeword LLR = 2 (1 + sigma z) / sigma^2 (awgn.py:47, :75, :88), so mean
+    2 / sigma^2 and variance 4 / sigma^2; z standard normal including both tails;
+    the two Box-Muller outputs of a pair uncorrelated; and a two-sample KS test
+    against np.random.normal (the reference's noise source)."""
+    from scipy import stats
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    snr = 1.0
+    ch = AWGNChannel(snr)
+    s2 = ch.noise_std ** 2
+    B, n = 4096, 1024
+    llr = ch.llr_batch_device(None, n, B, seed=77).double()
+    M = B * n
+    mean = llr.mean().item()
+    var = llr.var().item()
+    assert abs(mean / (2.0 / s2) - 1.0) < 5 * (math.sqrt(4.0 / s2 / M) / (2.0 / s2))
+    assert abs(var / (4.0 / s2) - 1.0) < 5 * math.sqrt(2.0 / M)
+    z = ((llr * s2 / 2.0 - 1.0) / ch.noise_std).flatten()
+    for t in (1.0, 2.0, 3.0, 4.0):
+        p = 2 * stats.norm.sf(t)
+        for side in (z > t, z < -t):
+            got = side.double().mean().item()
+            assert abs(got - p / 2) < 5 * math.sqrt(p / 2 / M) + 1e-7, (t, got, p / 2)
+    zz = z.view(B, n // 2, 2)
+    corr = torch.corrcoef(torch.stack([zz[..., 0].flatten(), zz[..., 1].flatten()]))[0, 1].item()
+    assert abs(corr) < 5 / math.sqrt(M / 2)
+    zs = z[:: 16].cpu().numpy()
+    rng = np.random.RandomState(5)
+    ks = stats.ks_2samp(zs, rng.normal(0.0, 1.0, size=zs.size))
+    assert ks.pvalue > 1e-3, ks
+    assert stats.kstest(zs, "norm").pvalue > 1e-3
+    # codeword signs: BPSK 0 -> +1, 1 -> -1 (awgn.py:47) on the same noise
+    cw = torch.ones((B, n), dtype=torch.uint8, device="cuda")
+    neg = ch.llr_batch_device(cw, n, B, seed=77)
+    assert torch.allclose(neg - (llr - 4.0 / s2), torch.zeros_like(neg), atol=1e-9 * (4.0 / s2))

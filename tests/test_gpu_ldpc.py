@@ -193,3 +193,40 @@ def test_empty_batch(gpu):
         assert bits.shape == (0, dec.n)
     bits, its = L.BPDecoder(H, max_iter=20).decode_batch(np.zeros((0, 504)), return_iterations=True)
     assert bits.shape == (0, 504) and its.shape == (0,)
+
+
+def test_global_workspace_two_streams(gpu, oracle):
+    """BP on an n=8192 code keeps its messages in a per-stream global workspace:
+    two streams sharing one plan (different batch sizes, so each stream's
+    workspace is sized to its own batch and regrown) decode exactly as serial
+    decodes, and a caller-supplied workspace of one frame gives the same bits."""
+    L = _L()
+    H = L.regular_construction(8192, 3, 6, seed=2)
+    dec = L.BPDecoder(H, max_iter=8)
+    plan = dec.plan
+    assert plan.info.reserved == 1  # generic kernel, global workspace
+    rng = np.random.RandomState(3)
+    xs = [torch.from_numpy(2.0 * (1.0 + 0.9 * rng.randn(B, 8192)) / 0.81).cuda() for B in (40, 72)]
+    want = [dec.decode_batch(x, return_iterations=True) for x in xs]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    got = [(torch.empty((x.shape[0], 8192), dtype=torch.uint8, device="cuda"),
+            torch.empty((x.shape[0],), dtype=torch.int32, device="cuda")) for x in xs]
+    for s in (s1, s2):
+        s.wait_stream(torch.cuda.current_stream())
+    for _ in range(2):
+        with torch.cuda.stream(s1):
+            plan.decode(xs[0], *got[0])
+        with torch.cuda.stream(s2):
+            plan.decode(xs[1], *got[1])
+    torch.cuda.synchronize()
+    for (b, i), (wb, wi) in zip(got, want):
+        assert torch.equal(b, wb) and torch.equal(i, wi)
+    unit = plan.workspace_bytes(1)
+    assert unit > 0 and plan.workspace_bytes(3) == 3 * unit
+    ws = torch.empty(unit, dtype=torch.uint8, device="cuda")
+    b, i = torch.empty_like(got[0][0]), torch.empty_like(got[0][1])
+    plan.decode(xs[0][:5], b[:5], i[:5], ws=ws)
+    assert torch.equal(b[:5], want[0][0][:5]) and torch.equal(i[:5], want[0][1][:5])
+    rp, ci = L.dense_to_csr(H)
+    wb, wi = oracle.ldpc_decode(rp, ci, 8192, xs[0][:4].cpu().numpy(), "bp", 8, True, 1.0, threads=4)
+    assert np.array_equal(b[:4].cpu().numpy(), wb) and np.array_equal(i[:4].cpu().numpy(), wi)

@@ -1,0 +1,82 @@
+"""BASELINE configs[4] at its full size on ONE GPU: 1 M frames of polar N=4096
+(4.3 G LLRs = 34 GB) and of LDPC n=8192 (8.6 G LLRs = 69 GB) -- past 2^32
+elements, so every frame / element index in the decoders, the channel and the
+error counter must be 64-bit.  Size-independent properties:
+  * frames far into the batch (LLR offsets > 2^32 elements) decode exactly as
+    the same rows decoded alone, and a sample matches the C oracle;
+  * the device error counter agrees with a recount of the decoded bits.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+FRAMES = 1 << 20
+
+
+def _rows(B):
+    # first rows, rows just past 2^32 elements of a 4096 / 8192 row pitch, last rows
+    return np.unique(np.r_[0:4, (1 << 20) - 8:(1 << 20), 1048000:1048004, 524288:524292, 786432:786436])
+
+
+def test_polar_n4096_l8_one_million_frames(gpu, oracle):
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.polar import SCLDecoder, construct_frozen_set
+    N, K, L, B = 4096, 2048, 8, FRAMES
+    fr = construct_frozen_set(N, K, 2.0)
+    dec = SCLDecoder(N, K, L, frozen_bits=fr)
+    msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    _native.random_bits(61, 0, msg)
+    cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+    _native.polar_encode(dec.plan, msg, cw)
+    llr = AWGNChannel(-1.0).llr_batch_device(cw, N, B, seed=62)
+    del cw
+    assert llr.numel() >= 2 ** 32
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    dec.plan.decode(llr, out)
+    counts = torch.zeros(3, dtype=torch.int64, device="cuda")
+    _native.count_errors(msg, out, K, counts)
+    err = (out != msg)
+    assert counts.tolist() == [int(err.sum().item()), int(err.any(dim=1).sum().item()), B]
+    rows = torch.from_numpy(_rows(B)).cuda()
+    alone = torch.empty((len(rows), K), dtype=torch.uint8, device="cuda")
+    dec.plan.decode(llr[rows].contiguous(), alone)
+    assert torch.equal(alone, out[rows])
+    pick = rows[-6:]
+    want = oracle.scl_decode(N, L, fr, llr[pick].cpu().numpy(), threads=16)
+    assert np.array_equal(out[pick].cpu().numpy().astype(np.int64), want)
+    del llr, out, msg, err
+    torch.cuda.empty_cache()
+
+
+def test_ldpc_n8192_ms_one_million_frames(gpu, oracle):
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.ldpc import MSDecoder, dense_to_csr
+    from polarcode_and_ldpc_amd.ldpc.matrix import regular_construction
+    n, B = 8192, FRAMES
+    H = regular_construction(n, 3, 6, seed=11)
+    k = n - H.shape[0]
+    dec = MSDecoder(H, max_iter=20, normalization=0.75)
+    llr = AWGNChannel(1.0).llr_batch_device(None, n, B, seed=63)
+    assert llr.numel() > 2 ** 33
+    out = torch.empty((B, n), dtype=torch.uint8, device="cuda")
+    its = torch.empty((B,), dtype=torch.int32, device="cuda")
+    dec.plan.decode(llr, out, its)
+    zero = torch.zeros((B, k), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(3, dtype=torch.int64, device="cuda")
+    _native.count_errors(zero, out, k, counts)
+    assert counts.tolist()[2] == B and counts.tolist()[0] == int(out[:, :k].sum().item())
+    rows = torch.from_numpy(_rows(B)).cuda()
+    alone, its1 = torch.empty((len(rows), n), dtype=torch.uint8, device="cuda"), torch.empty(
+        (len(rows),), dtype=torch.int32, device="cuda")
+    dec.plan.decode(llr[rows].contiguous(), alone, its1)
+    assert torch.equal(alone, out[rows]) and torch.equal(its1, its[rows])
+    pick = rows[-4:]
+    rp, ci = dense_to_csr(H)
+    want, _ = oracle.ldpc_decode(rp, ci, n, llr[pick].cpu().numpy(), "ms", 20, True, 0.75, threads=4)
+    assert np.array_equal(out[pick].cpu().numpy().astype(np.int64), want)
+    del llr, out, its, zero
+    torch.cuda.empty_cache()

@@ -103,3 +103,30 @@ def test_world2_equals_world1():
     assert one[2]["bit_errors"] == two[2]["bit_errors"]
     # low SNR point stops on max_errors
     assert one[0]["frame_errors"] >= 30 and two[0]["frame_errors"] >= 30
+
+
+def test_point_log_resume(tmp_path):
+    """An interrupted sweep resumes from its per-point JSON-lines log (SURVEY §5
+    checkpoint/resume) and gives exactly the uninterrupted counts; rows of
+    another configuration and a torn last line are ignored."""
+    from polarcode_and_ldpc_amd.harness.montecarlo import PointLog
+    snrs = [-5.0, 0.0, 4.0]
+    full = MonteCarlo(_cpu_round_fn(), info_bits=K, batch=24).run(snrs, num_frames=120, max_errors=30)
+    path = tmp_path / "points.jsonl"
+    key = dict(code="polar", N=N, K=K, frames=120, max_errors=30)
+    # "interrupted" after the first point, plus a foreign row and a torn line
+    MonteCarlo(_cpu_round_fn(), info_bits=K, batch=24).run(snrs[:1], 120, 30, log=PointLog(path, key))
+    PointLog(path, dict(key, frames=7)).append(full[2])
+    with open(path, "a") as f:
+        f.write('{"key": {"code": "pol')
+    calls = []
+    fn = _cpu_round_fn()
+
+    def counting(*a):
+        calls.append(a[0])
+        return fn(*a)
+
+    resumed = MonteCarlo(counting, info_bits=K, batch=24).run(snrs, 120, 30, log=PointLog(path, key))
+    assert 0 not in calls  # point 0 came from the log
+    assert [r.as_dict() for r in resumed] == [r.as_dict() for r in full]
+    assert len(PointLog(path, key).load()) == 3

@@ -47,6 +47,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 CLOCK_GHZ = 2.4
 
 
+SECTIONS = ("polar", "e2e", "ldpc", "ldpc_valid", "cascl", "sweep", "long_polar", "long_ms", "long_ms_noes")
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -262,7 +265,7 @@ def bench_polar(args, rt, pool):
                plan=dict(lds_bytes=plan.info.lds_bytes, fused_top=plan.info.fused_top),
                ber=float(c[0]) / max(1, c[2] * K), fer=float(c[1]) / max(1, c[2]), frames_counted=int(c[2]))
 
-    if not args.skip_extra:
+    if "e2e" in args.sec:
         # End-to-end Monte Carlo (SURVEY §8 d): fresh messages, encoding, AWGN,
         # decode and error count per step, all on the device.
         ch = AWGNChannel(args.snr)
@@ -343,7 +346,7 @@ def bench_ldpc(args, rt, pool):
                mean_iterations=float(its.double().mean().item()),
                roofline=roofline("ldpc_bp_504", kname, B, 9 * n, kms))
     res["roofline"]["limit"] = "VALU issue (fp64 transcendentals): see roofline.valu"
-    if not args.skip_extra:
+    if "ldpc_valid" in args.sec:
         # Second frame source (SURVEY §8 d): valid codewords (all-zero; BP is
         # codeword-symmetric) at the same SNR, early stop on.
         llr0 = AWGNChannel(args.snr).llr_batch_device(None, n, B, seed=4243, frame_offset=rt.rank * B)
@@ -407,7 +410,7 @@ def bench_cascl(args, rt):
                ber=float(c[0]) / max(1, c[2] * K), fer=float(c[1]) / max(1, c[2]),
                roofline=roofline("polar_cascl_1024_l32", polar_kernel_name(dec.plan, 10), B, 8 * N + K, kms))
     del llr, out, msg
-    if not args.skip_sweep:
+    if "sweep" in args.sec:
         t0 = time.perf_counter()
         snrs = np.arange(-2.0, 5.5, 1.0)
         _, _, pts = simulate_polar(snrs, args.sweep_frames, args.sweep_max_errors, {"encoding": {"N": N, "K": K}},
@@ -424,43 +427,54 @@ def bench_cascl(args, rt):
 
 def bench_long(args, rt):
     """BASELINE configs[4] per GPU: 1 M frames over 8 GPUs = 131 072 frames each."""
-    from polarcode_and_ldpc_amd import _native
-    from polarcode_and_ldpc_amd.channel import AWGNChannel
-    from polarcode_and_ldpc_amd.ldpc import MSDecoder
-    from polarcode_and_ldpc_amd.ldpc.matrix import regular_construction
     B = args.long_batch
     steps = min(args.steps, args.extra_steps)
     res = {}
+    if "long_polar" in args.sec:
+        res.update(_long_polar(rt, B, steps))
+    for es in (True, False):
+        if ("long_ms" if es else "long_ms_noes") in args.sec:
+            res.update(_long_ms(rt, B, steps, es))
+    return res
+
+
+def _long_polar(rt, B, steps):
     N, K = 4096, 2048
     dec, _, msg, llr = polar_fixture(rt, N, K, 8, B, 1.0, 45)
     out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
     dt, _, kms, c = decode_loop(rt, dec.plan, llr, out, msg, K, steps, 1)
-    res["polar_4096_l8"] = dict(
+    res = {"polar_4096_l8": dict(
         metric="decoded info-Mbps, polar N=4096 K=2048 SCL L=8 @ 1.0 dB", value=B * rt.world * steps * K / dt / 1e6,
         unit="info-Mbps", steps=steps, ms_per_step=dt / steps * 1e3, kernel_ms=kms, frames_per_gpu=B,
         llr_bytes_per_gpu=B * N * 8, fer=float(c[1]) / max(1, c[2]),
-        roofline=roofline("polar_scl_4096_l8", polar_kernel_name(dec.plan, 12), B, 8 * N + K, kms))
+        roofline=roofline("polar_scl_4096_l8", polar_kernel_name(dec.plan, 12), B, 8 * N + K, kms))}
     del dec, msg, llr, out
     torch.cuda.empty_cache()
+    return res
+
+
+def _long_ms(rt, B, steps, es):
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.ldpc import MSDecoder
+    from polarcode_and_ldpc_amd.ldpc.matrix import regular_construction
     n = 8192
     H = regular_construction(n, 3, 6, seed=11)  # every check degree 6 (min-sum needs >= 2)
     k = n - H.shape[0]
-    for es in (True, False):
-        dec = MSDecoder(H, max_iter=20, normalization=1.0, early_stop=es)
-        llr = AWGNChannel(1.5).llr_batch_device(None, n, B, seed=46, frame_offset=rt.rank * B)
-        out = torch.empty((B, n), dtype=torch.uint8, device="cuda")
-        its = torch.empty((B,), dtype=torch.int32, device="cuda")
-        zero = torch.zeros((B, k), dtype=torch.uint8, device="cuda")
-        dt, _, kms, c = decode_loop(rt, dec.plan, llr, out, zero, k, steps, 1, its)
-        res["ldpc_8192_ms20" + ("" if es else "_no_early_stop")] = dict(
-            metric="decoded info-Mbps, LDPC n=8192 (3,6)-regular min-sum max_iter=20, all-zero codeword @ 1.5 dB, "
-                   "early stop %s" % ("on" if es else "off"),
-            value=B * rt.world * steps * k / dt / 1e6, unit="info-Mbps", steps=steps, ms_per_step=dt / steps * 1e3,
-            kernel_ms=kms, frames_per_gpu=B, mean_iterations=float(its.double().mean().item()),
-            llr_bytes_per_gpu=B * n * 8, fer=float(c[1]) / max(1, c[2]),
-            roofline=roofline("ldpc_ms_8192" + ("" if es else "_noes"), "ldpc_ms_compact_kernel", B, 9 * n, kms))
-        del llr, out, its, zero, dec
-        torch.cuda.empty_cache()
+    dec = MSDecoder(H, max_iter=20, normalization=1.0, early_stop=es)
+    llr = AWGNChannel(1.5).llr_batch_device(None, n, B, seed=46, frame_offset=rt.rank * B)
+    out = torch.empty((B, n), dtype=torch.uint8, device="cuda")
+    its = torch.empty((B,), dtype=torch.int32, device="cuda")
+    zero = torch.zeros((B, k), dtype=torch.uint8, device="cuda")
+    dt, _, kms, c = decode_loop(rt, dec.plan, llr, out, zero, k, steps, 1, its)
+    res = {"ldpc_8192_ms20" + ("" if es else "_no_early_stop"): dict(
+        metric="decoded info-Mbps, LDPC n=8192 (3,6)-regular min-sum max_iter=20, all-zero codeword @ 1.5 dB, "
+               "early stop %s" % ("on" if es else "off"),
+        value=B * rt.world * steps * k / dt / 1e6, unit="info-Mbps", steps=steps, ms_per_step=dt / steps * 1e3,
+        kernel_ms=kms, frames_per_gpu=B, mean_iterations=float(its.double().mean().item()),
+        llr_bytes_per_gpu=B * n * 8, fer=float(c[1]) / max(1, c[2]),
+        roofline=roofline("ldpc_ms_8192" + ("" if es else "_noes"), "ldpc_ms_compact_kernel", B, 9 * n, kms))}
+    del llr, out, its, zero, dec
+    torch.cuda.empty_cache()
     return res
 
 
@@ -532,11 +546,22 @@ def main():
     ap.add_argument("--skip-configs", action="store_true", help="no configs[3]/[4] keys")
     ap.add_argument("--skip-sweep", action="store_true", help="no CA-SCL BER sweep")
     ap.add_argument("--skip-extra", action="store_true",
-                    help="only the headline decodes (no end-to-end / valid-codeword / configs[3,4] runs): profiling")
+                    help="only the headline decodes (no end-to-end / valid-codeword / configs[3,4] runs)")
+    ap.add_argument("--sections", default=None,
+                    help="comma list of " + ",".join(SECTIONS) + " (profiling passes: one kernel per section)")
     ap.add_argument("--cpu-stub", action="store_true", help="CPU/gloo plumbing check with a stub decode")
     args = ap.parse_args()
+    sec = set(SECTIONS) if args.sections is None else set(args.sections.split(","))
+    assert sec <= set(SECTIONS), "unknown section in --sections"
     if args.skip_extra:
-        args.skip_configs = True
+        sec &= {"polar", "ldpc"}
+    if args.skip_ldpc:
+        sec -= {"ldpc", "ldpc_valid"}
+    if args.skip_configs:
+        sec -= {"cascl", "sweep", "long_polar", "long_ms", "long_ms_noes"}
+    if args.skip_sweep:
+        sec.discard("sweep")
+    args.sec = sec
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(self_launch(args))
@@ -559,12 +584,13 @@ def main():
         from oracle import refnumpy as R
         pool = R.make_pool(cpu_processes())
     pol = bench_polar(args, rt, pool)
-    ldp = None if args.skip_ldpc else bench_ldpc(args, rt, pool)
+    ldp = bench_ldpc(args, rt, pool) if "ldpc" in args.sec else None
     if pool is not None:
         pool.close()
     extra = {}
-    if not args.skip_configs:
+    if "cascl" in args.sec:
         extra["cascl_l32"] = bench_cascl(args, rt)
+    if args.sec & {"long_polar", "long_ms", "long_ms_noes"}:
         extra["long_block"] = bench_long(args, rt)
     if rt.rank == 0:
         line = {

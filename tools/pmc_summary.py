@@ -1,69 +1,91 @@
-"""Summarise a tools/gpu_full.sh (or gpu_prof.sh) run into profiles/.
+"""Summarise a tools/gpu_profile.sh run into profiles/ and profiles/pmc_traffic.json.
 
-usage: python tools/pmc_summary.py <gpurun_out/full_TAG> <profiles/rNN_TAG>
+usage: python tools/pmc_summary.py <gpurun_out/prof_TAG> <profiles/rNN_TAG>
 
 Writes <dst>/kernel_stats.csv (rocprofv3 --kernel-trace --stats summary),
-<dst>/pmc_summary.json (per-kernel mean FETCH_SIZE / WRITE_SIZE per launch) and
-updates profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
+<dst>/pmc_summary.json (per-kernel mean counters per launch) and updates
+profiles/pmc_traffic.json, which bench.py reads for roofline.traffic /
+roofline.valu.  Counters are averaged over the launches of each kernel in the
+PMC runs (bench sections with one decode kernel each, tools/gpu_profile.sh).
 
-SQ_INSTS_VALU (wave-level VALU instructions) per launch is recorded too when the
-pmc_valu pass exists.
-HBM traffic per launch = 2 * FETCH_SIZE + WRITE_SIZE (rocprofv3 reports KiB;
-FETCH_SIZE counts 64 B per 128 B request on gfx950 -> doubled, as
-MI355X_MICROARCH.md "HBM" prescribes; WRITE_SIZE is taken as reported).
+HBM-side traffic per launch = 2 * FETCH_SIZE + WRITE_SIZE (rocprofv3 reports
+KiB; on gfx950 FETCH_SIZE counts 64 B per 128 B request -> doubled, as
+MI355X_MICROARCH.md "HBM" prescribes; WRITE_SIZE as reported).  Infinity-cache
+hits are counted too (the guide: they are not excluded), so this is traffic
+beyond L2, an upper bound on DRAM bytes.
+VALU: SQ_INSTS_VALU and its fp64 classes (ADD/MUL/FMA/TRANS _F64); bench.py
+prices fp64 instructions at 4 SIMD cycles per wave64 and the rest at 2.
 """
-import csv
 import collections
+import csv
 import json
 import os
 import shutil
 import sys
 
-KEYS = {  # bench.py traffic key -> kernel-name prefix
-    "polar_scl_1024_l8": "void pl::polar_tree_kernel<10, 8, false, 3, 7, false, 4>",
-    "ldpc_bp_504": "void pl::ldpc_reg_kernel<0, 3, 6, 2>",
+# bench.py pmc key -> (kernel-name prefix, frames per launch in gpu_profile.sh)
+KEYS = {
+    "polar_scl_1024_l8": ("pl::polar_tree_kernel<10, 8, false, 3, 7, false, 4>", 65536),
+    "ldpc_bp_504": ("pl::ldpc_reg_kernel<0, 3, 6, 2>", 65536),
+    "polar_cascl_1024_l32": ("pl::polar_tree_kernel<10, 32, false, 3, 7, false, 4>", 65536),
+    "polar_scl_4096_l8": ("pl::polar_tree_kernel<12, 8, false, 3, 9, false, 4>", 32768),
+    "ldpc_ms_8192_noes": ("pl::ldpc_ms_compact_kernel", 32768),
 }
+F64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
 
 
 def per_kernel(path):
     d = collections.defaultdict(list)
+    if not os.path.exists(path):
+        return {}
     for r in csv.DictReader(open(path)):
-        d[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+        name = r["Kernel_Name"].replace("void ", "").split("(")[0]
+        d[(name, r["Counter_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in d.items()}
 
 
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
-    for f in ("bench.json", "bench_trace.json"):
+    for f in ("bench_trace.json",):
         if os.path.exists(os.path.join(src, f)):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f))
-    fetch = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
-    write = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
-    vp = os.path.join(src, "pmc_valu", "run_counter_collection.csv")
-    valu = per_kernel(vp) if os.path.exists(vp) else {}
+    counters = {}
+    for p in ("fetch", "write", "valu", "mix", "l2"):
+        for (name, cname), v in per_kernel(os.path.join(src, "pmc_" + p, "run_counter_collection.csv")).items():
+            counters.setdefault(name, {})[cname] = v
     summ = {}
-    for (name, _), v in fetch.items():
-        w = write.get((name, "WRITE_SIZE"), 0.0)
-        summ[name] = dict(fetch_size_kib=v, write_size_kib=w,
-                          hbm_bytes_per_launch=2 * v * 1024 + w * 1024)
-        if (name, "SQ_INSTS_VALU") in valu:
-            summ[name]["valu_instr_per_launch"] = valu[(name, "SQ_INSTS_VALU")]
-            summ[name]["waves_per_launch"] = valu.get((name, "SQ_WAVES"))
-    json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+    for name, c in counters.items():
+        s = dict(c)
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            s["hbm_bytes_per_launch"] = 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
+        if all(k in c for k in F64):
+            s["valu_fp64_per_launch"] = sum(c[k] for k in F64)
+        hit, miss = c.get("TCC_HIT_sum"), c.get("TCC_MISS_sum")
+        if hit is not None and miss is not None and hit + miss > 0:
+            s["l2_hit_rate"] = hit / (hit + miss)
+        summ[name] = s
+    json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1, sort_keys=True)
     tp = os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_traffic.json")
-    traffic = json.load(open(tp)) if os.path.exists(tp) else {}
-    for key, prefix in KEYS.items():
+    traffic = {}
+    for key, (prefix, frames) in KEYS.items():
         for name, s in summ.items():
-            if name.startswith(prefix):
-                traffic[key] = dict(bytes_per_launch=s["hbm_bytes_per_launch"], source=os.path.join(dst, "pmc_summary.json"),
-                                    kernel=name.split("(")[0])
-                if "valu_instr_per_launch" in s:
-                    traffic[key]["valu_instr_per_launch"] = s["valu_instr_per_launch"]
-    json.dump(traffic, open(tp, "w"), indent=1)
-    for name, s in summ.items():
-        if s["hbm_bytes_per_launch"] > 1e6:
-            print("%-60s %10.3f GB/launch" % (name[:60], s["hbm_bytes_per_launch"] / 1e9))
+            if name.startswith(prefix) and "hbm_bytes_per_launch" in s:
+                t = dict(bytes_per_launch=s["hbm_bytes_per_launch"], frames=frames, kernel=name,
+                         source=os.path.join(dst, "pmc_summary.json"))
+                if "SQ_INSTS_VALU" in s:
+                    t["valu_per_launch"] = s["SQ_INSTS_VALU"]
+                if "valu_fp64_per_launch" in s:
+                    t["valu_fp64_per_launch"] = s["valu_fp64_per_launch"]
+                if "l2_hit_rate" in s:
+                    t["l2_hit_rate"] = s["l2_hit_rate"]
+                traffic[key] = t
+    json.dump(traffic, open(tp, "w"), indent=1, sort_keys=True)
+    for name, s in sorted(summ.items()):
+        if s.get("hbm_bytes_per_launch", 0) > 1e6:
+            print("%-70s %9.3f GB/launch  VALU %.3g (f64 %.3g)  L2 hit %.2f" % (
+                name[:70], s["hbm_bytes_per_launch"] / 1e9, s.get("SQ_INSTS_VALU", 0),
+                s.get("valu_fp64_per_launch", 0), s.get("l2_hit_rate", float("nan"))))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,134 @@
+"""A/B timing of experimental builds of libpolarldpc.so (diagnostic).
+
+usage: python tools/ab.py [--cases polar_l8,ldpc_bp] [--reps 3] LIB [LIB ...]
+
+Each LIB is loaded in its own process (PL_LIB_PATH); libs alternate `reps`
+times.  Per case: median kernel time over 10 launches (HIP events, after 2
+warmups) and a digest of the decoded bits, which must equal the first LIB's.
+Build a variant with e.g.
+  make -C polarcode_and_ldpc_amd/csrc OUT=$PWD/build/lib_x.so OBJDIR=$PWD/build/obj_x EXTRA=-DPL_EXP_X
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = ("polar_l8", "ldpc_bp", "polar_l32", "polar_4096", "ms_8192", "polar_sc")
+
+
+def worker(cases):
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import torch
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.polar import construct_frozen_set
+    torch.cuda.set_device(0)
+    res = {}
+
+    def timeit(fn):
+        for _ in range(2):
+            fn()
+        ts = []
+        for _ in range(10):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b))
+        return float(np.median(ts))
+
+    def digest(t):
+        x = t.to(torch.int64).flatten()
+        w = torch.arange(1, x.numel() + 1, device=x.device, dtype=torch.int64) % 1000003
+        return int((x * w).sum().item())
+
+    for case in cases:
+        if case.startswith("polar"):
+            N, L, B, snr = {"polar_l8": (1024, 8, 65536, 3.0), "polar_l32": (1024, 32, 16384, 1.0),
+                            "polar_4096": (4096, 8, 16384, 1.0), "polar_sc": (1024, 0, 65536, 3.0)}[case]
+            K = N // 2
+            fr = construct_frozen_set(N, K, 2.0)
+            mask = np.zeros(N, np.uint8)
+            mask[fr] = 1
+            plan = _native.polar_plan(N, K, mask, L)
+            msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+            _native.random_bits(42, 0, msg)
+            cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+            _native.polar_encode(plan, msg, cw)
+            llr = AWGNChannel(snr).llr_batch_device(cw, N, B, seed=42)
+            out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+            ms = timeit(lambda: plan.decode(llr, out))
+            res[case] = dict(ms=ms, digest=digest(out), errors=int((out != msg).any(dim=1).sum().item()))
+        elif case == "ldpc_bp":
+            from polarcode_and_ldpc_amd.ldpc import BPDecoder, LDPCEncoder
+            enc = LDPCEncoder(504, 252, dv=3, dc=6, seed=42)
+            plan = BPDecoder(enc.H, max_iter=20).plan
+            B = 65536
+            base = enc.encode_batch(np.random.RandomState(42).randint(0, 2, (4096, 252)))
+            cw = torch.from_numpy(np.tile(base, (B // 4096, 1)).astype(np.uint8)).cuda()
+            llr = AWGNChannel(3.0).llr_batch_device(cw, 504, B, seed=4242)
+            out = torch.empty((B, 504), dtype=torch.uint8, device="cuda")
+            its = torch.empty((B,), dtype=torch.int32, device="cuda")
+            ms = timeit(lambda: plan.decode(llr, out, its))
+            res[case] = dict(ms=ms, digest=digest(out) ^ digest(its))
+        elif case == "ms_8192":
+            from polarcode_and_ldpc_amd.ldpc import MSDecoder
+            from polarcode_and_ldpc_amd.ldpc.matrix import regular_construction
+            H = regular_construction(8192, 3, 6, seed=11)
+            plan = MSDecoder(H, max_iter=20, early_stop=False).plan
+            B = 16384
+            llr = AWGNChannel(1.5).llr_batch_device(None, 8192, B, seed=46)
+            out = torch.empty((B, 8192), dtype=torch.uint8, device="cuda")
+            its = torch.empty((B,), dtype=torch.int32, device="cuda")
+            ms = timeit(lambda: plan.decode(llr, out, its))
+            res[case] = dict(ms=ms, digest=digest(out))
+    print(json.dumps(res), flush=True)
+
+
+def main():
+    args = sys.argv[1:]
+    if args and args[0] == "--worker":
+        worker(args[1].split(","))
+        return
+    cases, reps = ["polar_l8", "ldpc_bp"], 3
+    libs = []
+    i = 0
+    while i < len(args):
+        if args[i] == "--cases":
+            cases = args[i + 1].split(",")
+            i += 2
+        elif args[i] == "--reps":
+            reps = int(args[i + 1])
+            i += 2
+        else:
+            libs.append(os.path.abspath(args[i]))
+            i += 1
+    table = {lib: {c: [] for c in cases} for lib in libs}
+    ref = {}
+    for r in range(reps):
+        for lib in libs:
+            env = dict(os.environ, PL_LIB_PATH=lib)
+            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--worker", ",".join(cases)], env=env,
+                               capture_output=True, text=True, timeout=600)
+            if p.returncode != 0:
+                print("FAIL", lib, p.stderr[-3000:], flush=True)
+                sys.exit(p.returncode)
+            res = json.loads(p.stdout.strip().splitlines()[-1])
+            for c, v in res.items():
+                table[lib][c].append(v["ms"])
+                if c not in ref:
+                    ref[c] = v["digest"]
+                elif v["digest"] != ref[c]:
+                    print("MISMATCH", os.path.basename(lib), c, flush=True)
+            print("rep %d %s %s" % (r, os.path.basename(lib), json.dumps(res)), flush=True)
+    print("%-40s %s" % ("lib", "  ".join("%12s" % c for c in cases)))
+    for lib in libs:
+        print("%-40s %s" % (os.path.basename(lib), "  ".join("%12.3f" % min(table[lib][c]) for c in cases)))
+
+
+if __name__ == "__main__":
+    main()

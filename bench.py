@@ -58,20 +58,27 @@ def log(*a):
 class Runtime:
     """One process per GPU (RCCL) or, with --cpu-stub, per CPU rank (gloo)."""
 
-    def __init__(self, stub: bool):
+    def __init__(self, stub: bool, backend: str = "nccl"):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.stub = stub
+        self.host_reduce = stub or backend == "gloo"
         if stub:
             self.device = torch.device("cpu")
             if self.world > 1:
                 dist.init_process_group("gloo")
         else:
-            torch.cuda.set_device(self.local)
-            self.device = torch.device("cuda", self.local)
+            # --dist-backend gloo: ranks may share a GPU (a rehearsal of the
+            # multi-rank path on a one-GPU box; RCCL refuses duplicate GPUs)
+            dev = self.local if backend == "nccl" else self.local % torch.cuda.device_count()
+            torch.cuda.set_device(dev)
+            self.device = torch.device("cuda", dev)
             if self.world > 1:
-                dist.init_process_group("nccl", device_id=self.device)
+                if backend == "nccl":
+                    dist.init_process_group("nccl", device_id=self.device)
+                else:
+                    dist.init_process_group("gloo")
 
     def sync(self):
         if not self.stub:
@@ -83,14 +90,19 @@ class Runtime:
 
     def all_reduce(self, t, op=None):
         if self.world > 1:
-            dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
+            if self.host_reduce and t.is_cuda:
+                h = t.cpu()
+                dist.all_reduce(h, op=op or dist.ReduceOp.SUM)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
         return t
 
     def gather(self, x: float):
         """x from every rank, rank order."""
-        t = torch.tensor([x], dtype=torch.float64, device=self.device)
         if self.world == 1:
             return [x]
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if self.host_reduce else self.device)
         out = [torch.zeros_like(t) for _ in range(self.world)]
         dist.all_gather(out, t)
         return [float(o.item()) for o in out]
@@ -550,6 +562,8 @@ def main():
     ap.add_argument("--sections", default=None,
                     help="comma list of " + ",".join(SECTIONS) + " (profiling passes: one kernel per section)")
     ap.add_argument("--cpu-stub", action="store_true", help="CPU/gloo plumbing check with a stub decode")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: host-side counter reduction, ranks may share one GPU (rehearsal only)")
     args = ap.parse_args()
     sec = set(SECTIONS) if args.sections is None else set(args.sections.split(","))
     assert sec <= set(SECTIONS), "unknown section in --sections"
@@ -566,7 +580,7 @@ def main():
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(self_launch(args))
 
-    rt = Runtime(args.cpu_stub)
+    rt = Runtime(args.cpu_stub, args.dist_backend)
     if args.cpu_stub:
         r = bench_stub(args, rt)
         if rt.rank == 0:

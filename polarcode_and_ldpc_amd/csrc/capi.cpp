@@ -241,12 +241,12 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     if (!g.use_global && !g.check_kernel && !(lk && std::string(lk) == "generic")) {
         bool regular = true;
         for (int v = 0; v < n && regular; ++v) regular = (var_ptr[v + 1] - var_ptr[v]) == maxdv;
-        if (regular && maxdv < 8) g.reg_variant = pl::ldpc_reg_variant(maxdv, E, n);
+        if (regular && maxdv < 8 && E < 65536) g.reg_variant = pl::ldpc_reg_variant(maxdv, E, n);
         if (g.reg_variant) {
             g.threads = 256;
-            // + the BP tanh work list: E indices + a counter (ldpc_reg_kernel)
+            // + the BP tanh work list: E 16-bit indices + a counter (ldpc_reg_kernel)
             const size_t base = ((size_t)2 * E * 8 + lds_small + 15) & ~(size_t)15;
-            g.lds_bytes = (int)((base + (size_t)4 * E + 16 + 15) & ~(size_t)15);
+            g.lds_bytes = (int)((base + (((size_t)2 * E + 3) & ~(size_t)3) + 16 + 15) & ~(size_t)15);
         }
     }
     // min-sum codes whose T/C arrays exceed LDS: compressed check state in LDS

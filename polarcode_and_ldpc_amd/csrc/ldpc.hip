@@ -242,8 +242,11 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
 // tid + j*256 (j < VPT); their edge metadata, var_edge / var_chk lists and
 // channel LLRs are loaded once into registers instead of once per iteration.
 // Same passes, barriers and arithmetic as ldpc_decode_kernel (bit-identical).
+#ifndef PL_LDPC_REG_WPE
+#define PL_LDPC_REG_WPE 4  // waves per SIMD the register budget is built for
+#endif
 template <int ALGO, int DV, int EPT, int VPT>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PL_LDPC_REG_WPE)))
 ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
                 uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -257,9 +260,11 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
     uint32_t* syn = reinterpret_cast<uint32_t*>(smem + (size_t)16 * E);  // [2][m]
     uint8_t* bt = reinterpret_cast<uint8_t*>(syn + 2 * m);               // [n]
     // BP: edges whose v2c needs a tanh (|x| <= 14.52 or NaN), compacted: [E]
-    // indices + a counter (ldpc_reg_lds_bytes)
-    int32_t* work = reinterpret_cast<int32_t*>(smem + (((size_t)16 * E + (size_t)8 * m + n + 15) & ~(size_t)15));
-    int32_t* wcnt = work + E;
+    // 16-bit edge indices (E < 65536) + a counter; 29 KB per frame at (504,252),
+    // so 5 frames fit a CU's LDS (capi.cpp sizes it)
+    uint16_t* work = reinterpret_cast<uint16_t*>(smem + (((size_t)16 * E + (size_t)8 * m + n + 15) & ~(size_t)15));
+    int32_t* wcnt = reinterpret_cast<int32_t*>(smem + ((((size_t)16 * E + (size_t)8 * m + n + 15) & ~(size_t)15) +
+                                                       (((size_t)2 * E + 3) & ~(size_t)3)));
     const double* __restrict__ ch = llr + frame * ld;
     auto tin = [&](double x) -> double { return ALGO == 0 ? tanh_half_clip(x) : x; };
     const int lane = __lane_id();
@@ -377,7 +382,7 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
                         base = __builtin_amdgcn_readlane(base, leader);
                         const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                        if (!sat) work[base + pre] = ve[j][k];
+                        if (!sat) work[base + pre] = (uint16_t)ve[j][k];
                     }
                 } else {
                     T[ve[j][k]] = x;

@@ -89,7 +89,9 @@ class MonteCarlo:
         if self.world == 1:
             return counts
         import torch
-        t = torch.as_tensor(counts, dtype=torch.int64, device=self.device)
+        # RCCL reduces device tensors; gloo (CPU tests, one-GPU rehearsals) host ones
+        dev = "cpu" if self._dist.get_backend(self.group) == "gloo" else self.device
+        t = torch.as_tensor(counts, dtype=torch.int64, device=dev)
         self._dist.all_reduce(t, group=self.group)
         return t.cpu().numpy()
 

@@ -250,6 +250,9 @@ def decode_loop(rt, plan, llr, out, msg, width, steps, warmup, iters=None):
 
     def step():
         kt(lambda: plan.decode(llr, out, iters))
+        if rt.world == 1:  # pl_count_errors accumulates: no per-step reduction needed
+            _native.count_errors(msg, out, width, counts)
+            return
         sc.zero_()
         _native.count_errors(msg, out, width, sc)
         rt.all_reduce(sc)

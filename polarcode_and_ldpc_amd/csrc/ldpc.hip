@@ -455,6 +455,9 @@ PL_DEV double ms_c2v(double2 mm, uint32_t meta, int i, double norm) {
 // total rides along), vote (early stop, as ldpc_check_kernel), variable pass
 // (thread = variable: total = llr + np.sum of the rebuilt c2v in the reference's
 // order).  Decisions total <= 0.
+// VPT > 0 (n <= 1024 * VPT): each thread keeps the channel LLRs of its
+// variables tid + 1024 j in registers instead of re-reading them every iteration.
+template <int VPT>
 __global__ void __launch_bounds__(1024)
 ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
                        uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch) {
@@ -469,6 +472,11 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
     const double* __restrict__ ch = llr + frame * ld;
     const int32_t* __restrict__ rp = dv.row_ptr;
     const int32_t* __restrict__ ci = dv.col_idx;
+    double chv[VPT > 0 ? VPT : 1];
+    if constexpr (VPT > 0) {
+#pragma unroll
+        for (int j = 0; j < VPT; ++j) chv[j] = tid + 1024 * j < n ? ch[tid + 1024 * j] : 0.0;
+    }
     for (int v = tid; v < n; v += nt) tot[v] = ch[v];
     __syncthreads();
     int done = g.max_iter;
@@ -508,7 +516,9 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
         } else {
             __syncthreads();
         }
-        for (int v = tid; v < n; v += nt) {
+#pragma unroll
+        for (int jv = 0; jv < (VPT > 0 ? VPT : 1); ++jv) {
+          for (int v = tid + 1024 * jv; v < n; v += (VPT > 0 ? n : nt)) {
             const int a0 = dv.var_ptr[v], d = dv.var_ptr[v + 1] - a0;
             const int32_t* __restrict__ cp = dv.var_cp + a0;
             auto c2v = [&](int k) -> double {
@@ -531,7 +541,8 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
                 sum = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
                 for (; k < d; ++k) sum += c2v(k);
             }
-            tot[v] = ch[v] + sum;
+            tot[v] = (VPT > 0 ? chv[jv] : ch[v]) + sum;
+          }
         }
         __syncthreads();
     }
@@ -644,7 +655,7 @@ static void* pick(bool global) {
 }
 
 static void* pick_kernel(const LdpcGeom& g) {
-    if (g.compact) return (void*)ldpc_ms_compact_kernel;
+    if (g.compact) return g.n <= 8192 ? (void*)ldpc_ms_compact_kernel<8> : (void*)ldpc_ms_compact_kernel<0>;
     if (g.reg_variant) {
         int cnt;
         return reg_table(cnt)[g.reg_variant - 1].k[g.algo == 0 ? 0 : 1];

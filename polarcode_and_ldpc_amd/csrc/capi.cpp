@@ -227,6 +227,9 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     pl::LdpcGeom& g = p->lg;
     g.m = m; g.n = n; g.E = E; g.max_iter = max_iter; g.early_stop = early_stop ? 1 : 0; g.algo = algo;
     g.maxdc = maxdc; g.maxdv = maxdv; g.norm = normalization;
+    g.regular = 1;
+    for (int c = 0; c < m && g.regular; ++c) g.regular = (row_ptr[c + 1] - row_ptr[c]) == maxdc;
+    for (int v = 0; v < n && g.regular; ++v) g.regular = (var_ptr[v + 1] - var_ptr[v]) == maxdv;
     g.threads = E <= 4096 ? 256 : 1024;
     if (E >= (1 << 20) || maxdc >= (1 << 11)) { delete p; return fail(PL_EUNSUPPORTED, "code too large"); }
     const size_t lds_small = (size_t)8 * m + n;                 // syndrome [2][m] u32 + decisions [n]

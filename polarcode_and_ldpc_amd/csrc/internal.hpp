@@ -75,6 +75,7 @@ struct LdpcGeom {
     int check_kernel;  // 1: ldpc_check_kernel (thread per check, state in LDS)
     int reg_variant;   // > 0: ldpc_reg_kernel instance (constant variable degree, LDS state)
     int compact;       // 1: ldpc_ms_compact_kernel (min-sum, compressed check state in LDS)
+    int regular;       // every check has degree maxdc and every variable degree maxdv
 };
 struct LdpcDev {
     const int32_t* row_ptr;   // [m+1]

@@ -457,7 +457,10 @@ PL_DEV double ms_c2v(double2 mm, uint32_t meta, int i, double norm) {
 // order).  Decisions total <= 0.
 // VPT > 0 (n <= 1024 * VPT): each thread keeps the channel LLRs of its
 // variables tid + 1024 j in registers instead of re-reading them every iteration.
-template <int VPT>
+// DV, DC > 0: a (DV, DC)-regular code (every variable / check degree equal, as
+// the BASELINE n = 8192 code): edge offsets are c * DC and v * DV, no row/column
+// pointer loads, and the edge loops unroll so their index loads issue together.
+template <int VPT, int DV, int DC>
 __global__ void __launch_bounds__(1024)
 ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
                        uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch) {
@@ -483,14 +486,20 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
     for (int it = 0; it < g.max_iter; ++it) {
         int syn = 0;
         for (int c = tid; c < m; c += nt) {
-            const int e0 = rp[c], d = rp[c + 1] - e0;
+            const int e0 = DC > 0 ? c * DC : rp[c], d = DC > 0 ? DC : rp[c + 1] - e0;
             const double2 om = smin[c];
             const uint32_t ometa = smeta[c];
             double min1 = __builtin_inf(), min2 = __builtin_inf();
             uint32_t idx1 = 0, ncnt = 0, nidx = 0, zcnt = 0, zidx = 0, par = 0, negs = 0;
             int s = 0;
-            for (int k = 0; k < d; ++k) {
-                const double tv = tot[ci[e0 + k]];
+            int cidx[DC > 0 ? DC : 1];
+            if constexpr (DC > 0) {
+#pragma unroll
+                for (int k = 0; k < DC; ++k) cidx[k] = ci[e0 + k];
+            }
+#pragma unroll
+            for (int k = 0; k < (DC > 0 ? DC : d); ++k) {
+                const double tv = tot[DC > 0 ? cidx[k] : ci[e0 + k]];
                 s ^= (tv <= 0.0) ? 1 : 0;
                 const double x = it == 0 ? tv : tv - ms_c2v(om, ometa, k, g.norm);
                 if (__builtin_isnan(x)) {
@@ -519,14 +528,22 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
 #pragma unroll
         for (int jv = 0; jv < (VPT > 0 ? VPT : 1); ++jv) {
           for (int v = tid + 1024 * jv; v < n; v += (VPT > 0 ? n : nt)) {
-            const int a0 = dv.var_ptr[v], d = dv.var_ptr[v + 1] - a0;
+            const int a0 = DV > 0 ? v * DV : dv.var_ptr[v], d = DV > 0 ? DV : dv.var_ptr[v + 1] - a0;
             const int32_t* __restrict__ cp = dv.var_cp + a0;
             auto c2v = [&](int k) -> double {
                 const int c = cp[k] >> 4;
                 return ms_c2v(smin[c], smeta[c], cp[k] & 15, g.norm);
             };
             double sum;
-            if (d < 8) {  // np.sum: sequential below 8 terms, pairwise (8 accumulators) above
+            if constexpr (DV > 0 && DV < 8) {  // sequential np.sum, loads issued together
+                int cpk[DV];
+#pragma unroll
+                for (int k = 0; k < DV; ++k) cpk[k] = cp[k];
+                sum = 0.0;
+#pragma unroll
+                for (int k = 0; k < DV; ++k)
+                    sum += ms_c2v(smin[cpk[k] >> 4], smeta[cpk[k] >> 4], cpk[k] & 15, g.norm);
+            } else if (d < 8) {  // np.sum: sequential below 8 terms, pairwise (8 accumulators) above
                 sum = 0.0;
                 for (int k = 0; k < d; ++k) sum += c2v(k);
             } else {
@@ -655,7 +672,10 @@ static void* pick(bool global) {
 }
 
 static void* pick_kernel(const LdpcGeom& g) {
-    if (g.compact) return g.n <= 8192 ? (void*)ldpc_ms_compact_kernel<8> : (void*)ldpc_ms_compact_kernel<0>;
+    if (g.compact) {
+        if (g.n <= 8192 && g.regular && g.maxdv == 3 && g.maxdc == 6) return (void*)ldpc_ms_compact_kernel<8, 3, 6>;
+        return g.n <= 8192 ? (void*)ldpc_ms_compact_kernel<8, 0, 0> : (void*)ldpc_ms_compact_kernel<0, 0, 0>;
+    }
     if (g.reg_variant) {
         int cnt;
         return reg_table(cnt)[g.reg_variant - 1].k[g.algo == 0 ? 0 : 1];

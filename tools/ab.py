@@ -1,6 +1,6 @@
 """A/B timing of experimental builds of libpolarldpc.so (diagnostic).
 
-usage: python tools/ab.py [--cases polar_l8,ldpc_bp] [--reps 3] LIB [LIB ...]
+usage: python tools/ab.py [--cases polar_l8,ldpc_bp] [--reps 3] LIB[@VAR=VAL,...] [...]
 
 Each LIB is loaded in its own process (PL_LIB_PATH); libs alternate `reps`
 times.  Per case: median kernel time over 10 launches (HIP events, after 2
@@ -105,13 +105,17 @@ def main():
             reps = int(args[i + 1])
             i += 2
         else:
-            libs.append(os.path.abspath(args[i]))
+            libs.append(args[i])
             i += 1
     table = {lib: {c: [] for c in cases} for lib in libs}
     ref = {}
     for r in range(reps):
         for lib in libs:
-            env = dict(os.environ, PL_LIB_PATH=lib)
+            path, _, extra = lib.partition("@")
+            env = dict(os.environ, PL_LIB_PATH=os.path.abspath(path))
+            for kv in filter(None, extra.split(",")):
+                k, _, v = kv.partition("=")
+                env[k] = v
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--worker", ",".join(cases)], env=env,
                                capture_output=True, text=True, timeout=600)
             if p.returncode != 0:

@@ -28,7 +28,7 @@ KEYS = {
     "polar_scl_1024_l8": ("pl::polar_tree_kernel<10, 8, false, 3, 7, false, 4>", 65536),
     "ldpc_bp_504": ("pl::ldpc_reg_kernel<0, 3, 6, 2>", 65536),
     "polar_cascl_1024_l32": ("pl::polar_tree_kernel<10, 32, false, 3, 7, false, 4>", 65536),
-    "polar_scl_4096_l8": ("pl::polar_tree_kernel<12, 8, false, 3, 9, false, 4>", 32768),
+    "polar_scl_4096_l8": ("pl::polar_tree_kernel<12, 8, false, 4, 9, false, 4>", 32768),
     "ldpc_ms_8192_noes": ("pl::ldpc_ms_compact_kernel", 32768),
 }
 F64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")

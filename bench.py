@@ -47,7 +47,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 CLOCK_GHZ = 2.4
 
 
-SECTIONS = ("polar", "e2e", "ldpc", "ldpc_valid", "cascl", "sweep", "long_polar", "long_ms", "long_ms_noes")
+SECTIONS = ("polar", "e2e", "polar_default", "ldpc", "ldpc_valid", "cascl", "sweep", "long_polar", "long_ms", "long_ms_noes")
 
 
 def log(*a):
@@ -221,8 +221,11 @@ def polar_fixture(rt, N, K, L, B, snr, seed, frozen_snr=2.0):
     from polarcode_and_ldpc_amd import _native
     from polarcode_and_ldpc_amd.channel import AWGNChannel
     from polarcode_and_ldpc_amd.polar import SCLDecoder, construct_frozen_set
-    frozen = construct_frozen_set(N, K, frozen_snr)
+    # frozen_snr None: the reference's default set (generate_frozen_bits, the
+    # decoders' frozen_bits=None case that throughput_test.py runs)
+    frozen = None if frozen_snr is None else construct_frozen_set(N, K, frozen_snr)
     dec = SCLDecoder(N, K, list_size=L, frozen_bits=frozen)
+    frozen = dec.frozen_bits
     off = rt.rank * B  # global frame indices: identical frames for any GPU count
     msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
     _native.random_bits(seed, off, msg)
@@ -311,6 +314,21 @@ def bench_polar(args, rt, pool):
                                       "SCL decode + error count (+ all-reduce)",
                                  ber=float(e[0]) / max(1, e[2] * K), fer=float(e[1]) / max(1, e[2]))
         del msg2, out2, cw2, llr2
+
+    if "polar_default" in args.sec:
+        # like-for-like with throughput_test.py (SURVEY §8 d): the default frozen
+        # set, info = indices whose bit reversal is >= N - K
+        dd, _, dmsg, dllr = polar_fixture(rt, N, K, L, B, args.snr, 47, frozen_snr=None)
+        dout = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+        ddt, _, dkms, dc = decode_loop(rt, dd.plan, dllr, dout, dmsg, K, args.steps, args.warmup)
+        res["default_frozen_set"] = dict(
+            metric="decoded info-Mbps, polar N=1024 K=512 SCL L=%d, reference default frozen set "
+                   "(generate_frozen_bits) @ %.1f dB" % (L, args.snr),
+            value=B * rt.world * args.steps * K / ddt / 1e6, unit="info-Mbps", ms_per_step=ddt / args.steps * 1e3,
+            kernel_ms=dkms, fer=float(dc[1]) / max(1, dc[2]),
+            roofline=roofline("polar_scl_1024_l8_default", polar_kernel_name(dd.plan, 10), B, 8 * N + K, dkms))
+        del dd, dmsg, dllr, dout
+        torch.cuda.empty_cache()
 
     if pool is not None:
         from oracle import oracle as O
@@ -624,6 +642,7 @@ def main():
             "cpu_baseline": pol.get("cpu_baseline"),
             "ber": pol["ber"], "fer": pol["fer"], "plan": pol["plan"],
             "end_to_end": pol.get("end_to_end"),
+            "default_frozen_set": pol.get("default_frozen_set"),
         }
         if ldp is not None:
             line["ldpc"] = ldp

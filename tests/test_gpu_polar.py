@@ -560,3 +560,26 @@ def test_caller_workspace_and_lazy_sizing(gpu):
         plan.decode(llr, wide[:, :512])
     with pytest.raises(AssertionError):
         plan.decode(llr.cpu(), out)
+
+
+def test_scl_default_frozen_set_vs_oracle(gpu, oracle):
+    """The reference's default frozen set (generate_frozen_bits: leaves 0..511
+    of the decode order frozen at N=1024, the set throughput_test.py runs and
+    bench.py's `default_frozen_set` line measures): HIP vs the C oracle, with
+    erasures and saturated LLRs mixed in."""
+    P = _P()
+    rng = np.random.RandomState(71)
+    enc = P.PolarEncoder(1024, 512)
+    B = 96
+    cw = enc.encode_batch(rng.randint(0, 2, (B, 512)))
+    snr = rng.uniform(-1.0, 3.0, size=(B, 1))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+    llr = 2.0 * ((1.0 - 2.0 * cw) + sigma * rng.randn(B, 1024)) / sigma ** 2
+    llr[5, :40] = 0.0
+    llr[6, 100:300] = np.inf
+    llr[7, ::3] = -np.inf
+    llr[8] = 0.0
+    for L in (8, 32):
+        want = oracle.scl_decode(1024, L, enc.frozen_bits, llr, threads=8)
+        got = P.SCLDecoder(1024, 512, list_size=L).decode_batch(llr)
+        assert _mismatch(got, want) == 0, L

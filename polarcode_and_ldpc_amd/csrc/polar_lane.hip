@@ -474,6 +474,7 @@ static void* lane_kernel(const LaneGeom& g, bool sc) {
         case 8: return lane_pick_f<8, false>(g.F, g.B);
         case 16: return lane_pick_f<16, false>(g.F, g.B);
         case 32: return lane_pick_f<32, false>(g.F, g.B);
+        case 64: return lane_pick_f<64, false>(g.F, g.B);  // one frame per wave
         default: return nullptr;
     }
 }

@@ -216,6 +216,21 @@ job_scl4096_wf_b = _job_scl4096_wf("job_scl4096_wf_b", -1.0, 212)
 ROUND2_JOBS = [job_scl1024_l32_m20, job_scl1024_l32_m10, job_scl1024_l32_m00, job_scl4096_wf_a, job_scl4096_wf_b]
 
 
+def job_scl_l64():
+    """Round 2: list size 64 (one frame per wavefront in the lane kernel), N=256
+    at 0/1/2 dB and N=1024 at 1 dB, bit-reversed Bhattacharyya sets."""
+    out = {}
+    for tag, (N, K, snrs, frames, seed) in (("N256", (256, 128, (0.0, 1.0, 2.0), 8, 301)),
+                                           ("N1024", (1024, 512, (1.0,), 4, 302))):
+        d = job_scl(N, K, 64, snrs, frames, seed, "x")[1]
+        for k in ("frozen", "llr", "msg", "snr", "scl", "ref_s_per_frame"):
+            out[tag + "_" + k] = d[k]
+    return "polar_scl_l64.npz", out
+
+
+ROUND2_JOBS.append(job_scl_l64)
+
+
 def job_small():
     """Small N, odd list sizes, K extremes, zero LLRs (deterministic cases)."""
     polar, _, channel = _imp()

@@ -223,7 +223,7 @@ def test_tree_kernel_ragged_batch(gpu):
 
 
 @pytest.mark.parametrize("N,L,crc,flags", [(1024, 32, "CRC-8", 0), (1024, 8, "CRC-16", 0), (1024, 8, "CRC-24", 0x20),
-                                           (256, 4, "CRC-8", 0), (4096, 8, "CRC-16", 0)])
+                                           (256, 4, "CRC-8", 0), (4096, 8, "CRC-16", 0), (256, 64, "CRC-8", 0)])
 def test_cascl_vs_oracle(gpu, oracle, N, L, crc, flags):
     """CRC-aided SCL (build-defined extension; the reference never applies its
     CRC, so parity is against the oracle's restatement of the same rule).  Frames
@@ -583,3 +583,25 @@ def test_scl_default_frozen_set_vs_oracle(gpu, oracle):
         want = oracle.scl_decode(1024, L, enc.frozen_bits, llr, threads=8)
         got = P.SCLDecoder(1024, 512, list_size=L).decode_batch(llr)
         assert _mismatch(got, want) == 0, L
+
+
+def test_scl_list_64_golden_and_oracle(gpu, oracle):
+    """List sizes 33..64 (lane kernel, one frame per wavefront): the reference's
+    L=64 fixture, plus non-power-of-two sizes and CA-SCL against the oracle."""
+    P = _P()
+    d = golden("polar_scl_l64.npz")
+    for tag, N in (("N256", 256), ("N1024", 1024)):
+        dec = P.SCLDecoder(N, N // 2, list_size=64, frozen_bits=d[tag + "_frozen"])
+        assert _mismatch(dec.decode_batch(d[tag + "_llr"]), d[tag + "_scl"]) == 0, tag
+    rng = np.random.RandomState(64)
+    N, K = 256, 128
+    fr = P.construct_frozen_set(N, K, 1.0)
+    cw = P.PolarEncoder(N, K, frozen_bits=fr).encode_batch(rng.randint(0, 2, (40, K)))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (rng.uniform(-1.0, 2.0, size=(40, 1)) / 10.0)))
+    llr = 2.0 * ((1.0 - 2.0 * cw) + sigma * rng.randn(40, N)) / sigma ** 2
+    llr[3, :30] = 0.0
+    for L in (33, 48, 64):
+        want = oracle.scl_decode(N, L, fr, llr, threads=8)
+        assert _mismatch(P.SCLDecoder(N, K, list_size=L, frozen_bits=fr).decode_batch(llr), want) == 0, L
+    with pytest.raises(ValueError):  # PL_EUNSUPPORTED: lists span one wavefront at most
+        P.SCLDecoder(N, K, list_size=65, frozen_bits=fr).decode_batch(llr)

@@ -139,6 +139,13 @@ def test_low_snr_large_list(oracle, name, N, L):
     assert _bad(oracle.scl_decode(N, L, d["frozen"], d["llr"], threads=8), d["scl"]) == 0
 
 
+def test_scl_l64(oracle):
+    """List size 64 (reference SCLDecoder, round-2 fixture)."""
+    d = golden("polar_scl_l64.npz")
+    for tag, N in (("N256", 256), ("N1024", 1024)):
+        assert _bad(oracle.scl_decode(N, 64, d[tag + "_frozen"], d[tag + "_llr"], threads=8), d[tag + "_scl"]) == 0
+
+
 def test_numpy_restatement_pinned():
     """oracle/refnumpy.py (the CPU baseline bench.py times as "the reference's
     NumPy path") reproduces the reference's outputs: SC / SCL on the config-1

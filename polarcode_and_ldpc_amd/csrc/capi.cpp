@@ -104,7 +104,7 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
         return fail(PL_EINVAL, "N must be a power of 2 in [2, 32768]");
     if (!(0 < K && K <= N)) return fail(PL_EINVAL, "K (info positions) must be in [1, N]");
     if (list_size < 0) return fail(PL_EINVAL, "list_size must be >= 1 (0 = SC)");
-    if (list_size > 64) return fail(PL_EUNSUPPORTED, "list_size > 64 not supported by this build (one wave per frame)");
+    if (list_size > 256) return fail(PL_EUNSUPPORTED, "list_size > 256 not supported by this build (8-bit path slots)");
     if (!frozen_mask) return fail(PL_EINVAL, "frozen_mask is NULL");
     int n = 0;
     while ((1 << n) < N) ++n;
@@ -149,7 +149,7 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
         pl::lane_geom(N, K, p->sc ? 1 : list_size, F, env_int("PL_POLAR_LDS_BUDGET", 8 * 1024), &p->lgeo);
         p->pg.F = p->lgeo.F;
         p->pg.lds_bytes = p->lgeo.lds_bytes;
-        p->fpw = 64 / p->lgeo.lcap;
+        p->fpw = p->lgeo.lcap >= 64 ? 1 : 64 / p->lgeo.lcap;
         p->ws_unit = (size_t)p->lgeo.ws_bytes;
         e = pl::lane_prepare(p->lgeo, p->sc, &per_cu);
     }

@@ -17,14 +17,16 @@ struct PolarGeom {
 // frames per wavefront; tree depths tiered over registers / LDS / workspace.
 struct LaneGeom {
     int N, n, K, Lsz, lcap, F, B, D, Dl, cw;
+    int lw;                        // lanes per workgroup: 64, or lcap (> 64: one frame per workgroup)
     int lds_bytes, lds_final;
-    int lds_pool[kMaxDepth + 2];   // byte offset of LDS pool depth d (Dl <= d <= D): [2^(n-d)][64] f64
-    int lds_bl[kMaxDepth + 2];     // byte offset of single-word beta depth d: [64] u32
+    int lds_xchg;                  // lcap > 64: metric / row / rank exchange scratch [lw]
+    int lds_pool[kMaxDepth + 2];   // byte offset of LDS pool depth d (Dl <= d <= D): [2^(n-d)][lw] f64
+    int lds_bl[kMaxDepth + 2];     // byte offset of single-word beta depth d: [lw] u32
     int bl_words[kMaxDepth + 2];   // beta words per slot at depth d
     int64_t ws_pool[kMaxDepth + 2];  // workspace byte offset of pool depth d (F <= d < Dl)
-    int64_t ws_bl[kMaxDepth + 2];    // workspace byte offset of multi-word beta depth d: [words][64] u32
-    int64_t ws_walk;                 // [2][cw][64] u32 walk buffers
-    int64_t ws_bytes;                // workspace bytes per wavefront
+    int64_t ws_bl[kMaxDepth + 2];    // workspace byte offset of multi-word beta depth d: [words][lw] u32
+    int64_t ws_walk;                 // [2][cw][lw] u32 walk buffers
+    int64_t ws_bytes;                // workspace bytes per workgroup
 };
 int lane_geom(int N, int K, int list_size, int F, int lds_budget, LaneGeom* g);
 hipError_t lane_prepare(const LaneGeom& g, bool sc, int* max_blocks_per_cu);

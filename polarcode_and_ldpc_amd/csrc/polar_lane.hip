@@ -81,24 +81,25 @@ PL_DEV void wave_fence() {
 struct Ctx {
     const LaneGeom* g;
     unsigned char* smem;
-    unsigned char* ws;  // this wave's global workspace
+    unsigned char* ws;  // this workgroup's global workspace
     int lane, base;     // base = first lane of this frame's group
+    int lw;             // lanes per workgroup (the stride of every lane-interleaved array)
 };
 
 // element t of lane-slot s at pool depth d (tier by d)
 PL_DEV double* pool(const Ctx& c, int d, int t, int s) {
     const LaneGeom& g = *c.g;
-    if (d >= g.Dl) return reinterpret_cast<double*>(c.smem + g.lds_pool[d]) + t * 64 + s;
-    return reinterpret_cast<double*>(c.ws + g.ws_pool[d]) + (size_t)t * 64 + s;
+    if (d >= g.Dl) return reinterpret_cast<double*>(c.smem + g.lds_pool[d]) + t * c.lw + s;
+    return reinterpret_cast<double*>(c.ws + g.ws_pool[d]) + (size_t)t * c.lw + s;
 }
 // word w of the beta array of lane-slot s at depth d
 PL_DEV uint32_t* blw(const Ctx& c, int d, int w, int s) {
     const LaneGeom& g = *c.g;
     if (g.bl_words[d] == 1) return reinterpret_cast<uint32_t*>(c.smem + g.lds_bl[d]) + s;
-    return reinterpret_cast<uint32_t*>(c.ws + g.ws_bl[d]) + (size_t)w * 64 + s;
+    return reinterpret_cast<uint32_t*>(c.ws + g.ws_bl[d]) + (size_t)w * c.lw + s;
 }
 PL_DEV uint32_t* walkbuf(const Ctx& c, int par, int w) {
-    return reinterpret_cast<uint32_t*>(c.ws + c.g->ws_walk) + ((size_t)par * c.g->cw + w) * 64 + c.lane;
+    return reinterpret_cast<uint32_t*>(c.ws + c.g->ws_walk) + ((size_t)par * c.g->cw + w) * c.lw + c.lane;
 }
 
 // child depth cd (size S = 2^(n-cd)) from parent depth cd-1 in lane-slot ps, own
@@ -108,6 +109,7 @@ template <bool PLDS, bool CLDS>
 PL_DEV void level(const Ctx& c, int cd, bool right, int ps, int bs, int os) {
     const LaneGeom& g = *c.g;
     const int S = 1 << (g.n - cd);
+    const int lw = c.lw;
     const double* __restrict__ P = PLDS ? reinterpret_cast<const double*>(c.smem + g.lds_pool[cd - 1]) + ps
                                         : reinterpret_cast<const double*>(c.ws + g.ws_pool[cd - 1]) + ps;
     double* __restrict__ C = CLDS ? reinterpret_cast<double*>(c.smem + g.lds_pool[cd]) + os
@@ -116,8 +118,8 @@ PL_DEV void level(const Ctx& c, int cd, bool right, int ps, int bs, int os) {
     if (S < U) {
         uint32_t bw = right ? *blw(c, cd, 0, bs) : 0u;
         for (int t = 0; t < S; ++t) {
-            const double a = P[2 * t * 64], b = P[(2 * t + 1) * 64];
-            C[t * 64] = right ? g_op(a, b, bw >> t) : f_ms(a, b);
+            const double a = P[2 * t * lw], b = P[(2 * t + 1) * lw];
+            C[t * lw] = right ? g_op(a, b, bw >> t) : f_ms(a, b);
         }
         return;
     }
@@ -125,12 +127,12 @@ PL_DEV void level(const Ctx& c, int cd, bool right, int ps, int bs, int os) {
         double a[U], b[U];
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            a[k] = P[(2 * (t0 + k)) * 64];
-            b[k] = P[(2 * (t0 + k) + 1) * 64];
+            a[k] = P[(2 * (t0 + k)) * lw];
+            b[k] = P[(2 * (t0 + k) + 1) * lw];
         }
         const uint32_t bw = right ? (*blw(c, cd, t0 >> 5, bs) >> (t0 & 31)) : 0u;
 #pragma unroll
-        for (int k = 0; k < U; ++k) C[(t0 + k) * 64] = right ? g_op(a[k], b[k], bw >> k) : f_ms(a[k], b[k]);
+        for (int k = 0; k < U; ++k) C[(t0 + k) * lw] = right ? g_op(a[k], b[k], bw >> k) : f_ms(a[k], b[k]);
     }
 }
 
@@ -169,7 +171,7 @@ PL_DEV double fused_top(const Ctx& c, int i, const double* __restrict__ ch, cons
             for (int k = 0; k < (1 << (F - d)); ++k)
                 v[k] = right[d] ? g_op(v[2 * k], v[2 * k + 1], bw >> k) : f_ms(v[2 * k], v[2 * k + 1]);
         }
-        if (F < n) C[(size_t)t * 64] = v[0];
+        if (F < n) C[(size_t)t * c.lw] = v[0];
         else lam = v[0];
     }
     return lam;
@@ -177,13 +179,17 @@ PL_DEV double fused_top(const Ctx& c, int i, const double* __restrict__ ch, cons
 
 }  // namespace
 
+// LCAP <= 64: 64/LCAP frames per wavefront, list exchanges by ds_bpermute.
+// LCAP > 64: one frame per workgroup of LCAP lanes (LCAP/64 wavefronts), list
+// exchanges through LDS (g.lds_xchg) behind workgroup barriers.
 template <int LCAP, bool SC, int F, int B>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(LCAP > 64 ? LCAP : 64)
 polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_t* __restrict__ out,
                   const uint32_t* __restrict__ frozen_dec, const int32_t* __restrict__ info_pos, int64_t batch,
                   unsigned char* __restrict__ workspace, const uint32_t* __restrict__ crc_g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int FPW = 64 / LCAP;
+    constexpr int FPW = LCAP >= 64 ? 1 : 64 / LCAP;
+    constexpr int LW = LCAP > 64 ? LCAP : 64;  // lanes per workgroup
     const int lane = threadIdx.x;
     const int fw = lane / LCAP, slot = lane % LCAP;
     const int n = g.n, N = g.N;
@@ -194,6 +200,7 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
     c.ws = workspace + (size_t)blockIdx.x * g.ws_bytes;
     c.lane = lane;
     c.base = fw * LCAP;
+    c.lw = LW;
 
     for (int64_t f0 = (int64_t)blockIdx.x * FPW; f0 < batch; f0 += (int64_t)gridDim.x * FPW) {
         const int64_t frame = f0 + fw;
@@ -234,7 +241,7 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                 if (D < c.g->Dl) __syncthreads();  // bottom node in the workspace (tiny LDS budget)
                 const double* node = pool(c, D, 0, src);
 #pragma unroll
-                for (int k = 0; k < (1 << B); ++k) v[k] = node[k * 64];
+                for (int k = 0; k < (1 << B); ++k) v[k] = node[k * LW];
 #pragma unroll
                 for (int s = 0; s < B; ++s) {
                     const int d = D + 1 + s;
@@ -260,6 +267,46 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
             } else {
                 double m0, m1;
                 path_metrics<true>(pm, lam, m0, m1);
+                const int nsurv = (2 * nact < g.Lsz) ? 2 * nact : g.Lsz;
+              if constexpr (LCAP > 64) {
+                // the same ranks through LDS: publish (m0, m1) and the pointer
+                // row, rank against every active path, publish the ranks, find
+                // the candidate this slot receives
+                double2* const xm = reinterpret_cast<double2*>(smem + g.lds_xchg);
+                uint64_t* const xr = reinterpret_cast<uint64_t*>(xm + LW);
+                int2* const xk = reinterpret_cast<int2*>(xr + 4 * LW);
+                xm[lane] = make_double2(m0, m1);
+                xr[4 * lane] = row.a0; xr[4 * lane + 1] = row.a1;
+                xr[4 * lane + 2] = row.b0; xr[4 * lane + 3] = row.b1;
+                __syncthreads();
+                int r0 = 0, r1 = 0;
+                for (int q = 0; q < nact; ++q) {
+                    const double2 v = xm[q];
+                    r0 += (v.x > m0) | ((v.x == m0) & (q < slot));
+                    r0 += v.y > m0;
+                    r1 += v.x >= m1;
+                    r1 += (v.y > m1) | ((v.y == m1) & (q < slot));
+                }
+                xk[lane] = make_int2(r0, r1);
+                __syncthreads();
+                int par = 0;
+                bit = 0;
+                for (int q = 0; q < nact; ++q) {
+                    const int2 k = xk[q];
+                    if (k.x == slot) { par = q; bit = 0; }
+                    if (k.y == slot) { par = q; bit = 1; }
+                }
+                if (slot < nsurv) {
+                    const double2 pv = xm[par];
+                    pm = bit ? pv.y : pv.x;
+                    row.a0 = xr[4 * par]; row.a1 = xr[4 * par + 1];
+                    row.b0 = xr[4 * par + 2]; row.b1 = xr[4 * par + 3];
+                } else {
+                    pm = -INFINITY;
+                }
+                nact = nsurv;
+                __syncthreads();  // exchange reads done before the next leaf's writes
+              } else {
                 // rank of (slot, b) in the stable descending order of
                 // [(m0, p) for active p] + [(m1, p) for active p]; all lane fetches of
                 // a chunk are issued before use (one LDS-crossbar round trip per chunk)
@@ -282,7 +329,6 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                         r1 += v & ((b[k] > m1) | ((b[k] == m1) & (q < slot)));
                     }
                 }
-                const int nsurv = (2 * nact < g.Lsz) ? 2 * nact : g.Lsz;
                 int par = 0;
                 bit = 0;
                 for (int q0 = 0; q0 < nact; q0 += QC) {
@@ -311,6 +357,7 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                     pm = -INFINITY;
                 }
                 nact = nsurv;
+              }
             }
 
             // -------------------------------------------- partial-sum walk
@@ -352,16 +399,44 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                 }
                 if (dd > 0) fill_pair(row.b0, row.b1, dd, dd + 1, slot);
             }
-            wave_fence();  // LDS is in order within a wave; only stop compiler reordering
+            if constexpr (LCAP > 64) __syncthreads();  // other wavefronts' beta words
+            else wave_fence();  // LDS is in order within a wave; only stop compiler reordering
         }
 
         // ------------------------------------------------ best path, output
         int best = 0;
-        if constexpr (!SC) {
+        if constexpr (!SC && LCAP > 64) {
+            double* const xp = reinterpret_cast<double*>(smem + g.lds_xchg);
+            uint32_t* const xkey = reinterpret_cast<uint32_t*>(xp + LW);
+            xp[lane] = pm;
+            __syncthreads();  // also: root partial sums in the workspace
+            if (crc_g) {
+                const uint32_t crc = crc_of_xhat(walkbuf(c, root_par, 0), LW, g.cw, crc_g);
+                int rank = 0;
+                for (int q = 0; q < nact; ++q) {
+                    const double v = xp[q];
+                    rank += (v > pm) | ((v == pm) & (q < slot));
+                }
+                xkey[lane] = slot >= nact ? 0xFFFFFFFFu : (uint32_t)(crc == 0u ? rank : LW + rank);
+                __syncthreads();
+                uint32_t bk = xkey[0];
+                for (int q = 1; q < nact; ++q) {
+                    const uint32_t k = xkey[q];
+                    if (k < bk) { bk = k; best = q; }
+                }
+            } else {
+                double bm = xp[0];
+                for (int q = 1; q < nact; ++q) {
+                    const double v = xp[q];
+                    if (v > bm) { bm = v; best = q; }
+                }
+            }
+            __syncthreads();  // scratch reads done before X (which may alias nothing) is written
+        } else if constexpr (!SC) {
             if (crc_g) {
                 // CRC-aided selection, as polar_tree.hip
                 __syncthreads();  // root partial sums in the workspace
-                const uint32_t crc = crc_of_xhat(walkbuf(c, root_par, 0), 64, g.cw, crc_g);
+                const uint32_t crc = crc_of_xhat(walkbuf(c, root_par, 0), LW, g.cw, crc_g);
                 int rank = 0;
                 for (int q = 0; q < LCAP; ++q) {
                     const double v = bperm_d(c.base + q, pm);
@@ -413,25 +488,29 @@ int lane_geom(int N, int K, int list_size, int F, int lds_budget, LaneGeom* g) {
     if (F < 1) F = 1;
     *g = LaneGeom{};
     g->N = N; g->n = n; g->K = K; g->Lsz = list_size < 1 ? 1 : list_size; g->lcap = lcap;
+    g->lw = lcap > 64 ? lcap : 64;
     g->F = F; g->B = lane_bottom(n, F); g->D = n - g->B;
     g->cw = N / 32 < 1 ? 1 : N / 32;
-    const int fpw = 64 / lcap;
-    // LDS: single-word beta depths + final transform buffer + pool depths [Dl, D]
+    const int fpw = lcap >= 64 ? 1 : 64 / lcap;
+    const int lw = g->lw;
+    // LDS: single-word beta depths + final transform buffer (+ list exchange
+    // scratch for lcap > 64: (m0, m1), pointer row, ranks per lane) + pool depths [Dl, D]
     int lds = 0;
     for (int d = 1; d <= n; ++d) {
         const int w = (1 << (n - d)) / 32;
         g->bl_words[d] = w < 1 ? 1 : w;
-        if (g->bl_words[d] == 1) { g->lds_bl[d] = lds; lds += 64 * 4; }
+        if (g->bl_words[d] == 1) { g->lds_bl[d] = lds; lds += lw * 4; }
     }
     g->lds_final = lds; lds += fpw * g->cw * 4;
     lds = (lds + 15) & ~15;
+    if (lcap > 64) { g->lds_xchg = lds; lds += lw * (16 + 32 + 8); }
     int Dl = g->D + 1;
     if (g->B > 0) {
         // deepest depths first, while they fit the LDS budget
-        while (Dl - 1 >= F && lds + (1 << (n - (Dl - 1))) * 64 * 8 <= lds_budget) {
+        while (Dl - 1 >= F && lds + (1 << (n - (Dl - 1))) * lw * 8 <= lds_budget) {
             --Dl;
             g->lds_pool[Dl] = lds;
-            lds += (1 << (n - Dl)) * 64 * 8;
+            lds += (1 << (n - Dl)) * lw * 8;
         }
     }
     g->Dl = Dl;
@@ -439,10 +518,10 @@ int lane_geom(int N, int K, int list_size, int F, int lds_budget, LaneGeom* g) {
     // workspace per wave: pool depths [F, Dl), multi-word beta depths, walk buffers
     int64_t ws = 0;
     if (g->B > 0)
-        for (int d = F; d < Dl; ++d) { g->ws_pool[d] = ws; ws += (int64_t)(1 << (n - d)) * 64 * 8; }
+        for (int d = F; d < Dl; ++d) { g->ws_pool[d] = ws; ws += (int64_t)(1 << (n - d)) * lw * 8; }
     for (int d = 1; d <= n; ++d)
-        if (g->bl_words[d] > 1) { g->ws_bl[d] = ws; ws += (int64_t)g->bl_words[d] * 64 * 4; }
-    g->ws_walk = ws; ws += (int64_t)2 * g->cw * 64 * 4;
+        if (g->bl_words[d] > 1) { g->ws_bl[d] = ws; ws += (int64_t)g->bl_words[d] * lw * 4; }
+    g->ws_walk = ws; ws += (int64_t)2 * g->cw * lw * 4;
     g->ws_bytes = (ws + 255) & ~(int64_t)255;
     return g->lds_bytes;
 }
@@ -474,7 +553,9 @@ static void* lane_kernel(const LaneGeom& g, bool sc) {
         case 8: return lane_pick_f<8, false>(g.F, g.B);
         case 16: return lane_pick_f<16, false>(g.F, g.B);
         case 32: return lane_pick_f<32, false>(g.F, g.B);
-        case 64: return lane_pick_f<64, false>(g.F, g.B);  // one frame per wave
+        case 64: return lane_pick_f<64, false>(g.F, g.B);    // one frame per wave
+        case 128: return lane_pick_f<128, false>(g.F, g.B);  // one frame per workgroup of 2 waves
+        case 256: return lane_pick_f<256, false>(g.F, g.B);  // 4 waves
         default: return nullptr;
     }
 }
@@ -485,7 +566,7 @@ hipError_t lane_prepare(const LaneGeom& g, bool sc, int* max_blocks_per_cu) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds_bytes);
     if (e != hipSuccess) return e;
     int nb = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64, g.lds_bytes);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, g.lw, g.lds_bytes);
     if (e != hipSuccess) return e;
     *max_blocks_per_cu = nb < 1 ? 1 : nb;
     return hipSuccess;
@@ -499,7 +580,7 @@ hipError_t lane_launch(const LaneGeom& g, bool sc, const double* llr, int64_t ld
     LaneGeom gg = g;
     void* args[] = {&gg, (void*)&llr, (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos, (void*)&batch,
                     (void*)&ws, (void*)&crc_g};
-    return hipLaunchKernel(k, dim3((unsigned)grid), dim3(64), args, g.lds_bytes, s);
+    return hipLaunchKernel(k, dim3((unsigned)grid), dim3((unsigned)g.lw), args, g.lds_bytes, s);
 }
 
 }  // namespace pl

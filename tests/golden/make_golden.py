@@ -231,6 +231,21 @@ def job_scl_l64():
 ROUND2_JOBS.append(job_scl_l64)
 
 
+def job_scl_l256():
+    """Round 2: list sizes 128 and 256 (one frame per multi-wavefront workgroup)."""
+    out = {}
+    for tag, (N, K, L, snrs, frames, seed) in (("N256_L128", (256, 128, 128, (0.0, 1.5), 4, 311)),
+                                              ("N256_L256", (256, 128, 256, (0.5,), 3, 312)),
+                                              ("N1024_L128", (1024, 512, 128, (1.0,), 2, 313))):
+        d = job_scl(N, K, L, snrs, frames, seed, "x")[1]
+        for k in ("frozen", "llr", "msg", "snr", "scl", "ref_s_per_frame"):
+            out[tag + "_" + k] = d[k]
+    return "polar_scl_l256.npz", out
+
+
+ROUND2_JOBS.append(job_scl_l256)
+
+
 def job_small():
     """Small N, odd list sizes, K extremes, zero LLRs (deterministic cases)."""
     polar, _, channel = _imp()

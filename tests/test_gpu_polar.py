@@ -223,7 +223,8 @@ def test_tree_kernel_ragged_batch(gpu):
 
 
 @pytest.mark.parametrize("N,L,crc,flags", [(1024, 32, "CRC-8", 0), (1024, 8, "CRC-16", 0), (1024, 8, "CRC-24", 0x20),
-                                           (256, 4, "CRC-8", 0), (4096, 8, "CRC-16", 0), (256, 64, "CRC-8", 0)])
+                                           (256, 4, "CRC-8", 0), (4096, 8, "CRC-16", 0), (256, 64, "CRC-8", 0),
+                                           (256, 128, "CRC-8", 0), (1024, 256, "CRC-16", 0)])
 def test_cascl_vs_oracle(gpu, oracle, N, L, crc, flags):
     """CRC-aided SCL (build-defined extension; the reference never applies its
     CRC, so parity is against the oracle's restatement of the same rule).  Frames
@@ -585,13 +586,18 @@ def test_scl_default_frozen_set_vs_oracle(gpu, oracle):
         assert _mismatch(got, want) == 0, L
 
 
-def test_scl_list_64_golden_and_oracle(gpu, oracle):
-    """List sizes 33..64 (lane kernel, one frame per wavefront): the reference's
-    L=64 fixture, plus non-power-of-two sizes and CA-SCL against the oracle."""
+def test_scl_large_lists_golden_and_oracle(gpu, oracle):
+    """List sizes 33..256 (lane kernel: one frame per wavefront up to 64, one
+    frame per workgroup of L/64 wavefronts above): the reference's L=64/128/256
+    fixtures, plus non-power-of-two sizes against the oracle."""
     P = _P()
     d = golden("polar_scl_l64.npz")
     for tag, N in (("N256", 256), ("N1024", 1024)):
         dec = P.SCLDecoder(N, N // 2, list_size=64, frozen_bits=d[tag + "_frozen"])
+        assert _mismatch(dec.decode_batch(d[tag + "_llr"]), d[tag + "_scl"]) == 0, tag
+    d = golden("polar_scl_l256.npz")
+    for tag, N, L in (("N256_L128", 256, 128), ("N256_L256", 256, 256), ("N1024_L128", 1024, 128)):
+        dec = P.SCLDecoder(N, N // 2, list_size=L, frozen_bits=d[tag + "_frozen"])
         assert _mismatch(dec.decode_batch(d[tag + "_llr"]), d[tag + "_scl"]) == 0, tag
     rng = np.random.RandomState(64)
     N, K = 256, 128
@@ -600,8 +606,13 @@ def test_scl_list_64_golden_and_oracle(gpu, oracle):
     sigma = np.sqrt(1.0 / (2.0 * 10 ** (rng.uniform(-1.0, 2.0, size=(40, 1)) / 10.0)))
     llr = 2.0 * ((1.0 - 2.0 * cw) + sigma * rng.randn(40, N)) / sigma ** 2
     llr[3, :30] = 0.0
-    for L in (33, 48, 64):
+    for L in (33, 48, 64, 65, 100, 128, 200, 256):
         want = oracle.scl_decode(N, L, fr, llr, threads=8)
         assert _mismatch(P.SCLDecoder(N, K, list_size=L, frozen_bits=fr).decode_batch(llr), want) == 0, L
-    with pytest.raises(ValueError):  # PL_EUNSUPPORTED: lists span one wavefront at most
-        P.SCLDecoder(N, K, list_size=65, frozen_bits=fr).decode_batch(llr)
+    fr64 = P.construct_frozen_set(64, 32, 1.0)
+    cw = P.PolarEncoder(64, 32, frozen_bits=fr64).encode_batch(rng.randint(0, 2, (24, 32)))
+    llr64 = 2.0 * ((1.0 - 2.0 * cw) + 1.2 * rng.randn(24, 64)) / 1.44
+    want = oracle.scl_decode(64, 256, fr64, llr64, threads=8)  # list outgrows 2^K paths: never pruned early
+    assert _mismatch(P.SCLDecoder(64, 32, list_size=256, frozen_bits=fr64).decode_batch(llr64), want) == 0
+    with pytest.raises(ValueError):  # PL_EUNSUPPORTED: 8-bit path slots
+        P.SCLDecoder(N, K, list_size=257, frozen_bits=fr).decode_batch(llr)

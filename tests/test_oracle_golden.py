@@ -146,6 +146,13 @@ def test_scl_l64(oracle):
         assert _bad(oracle.scl_decode(N, 64, d[tag + "_frozen"], d[tag + "_llr"], threads=8), d[tag + "_scl"]) == 0
 
 
+def test_scl_l128_l256(oracle):
+    """List sizes 128 and 256 (reference SCLDecoder, round-2 fixture)."""
+    d = golden("polar_scl_l256.npz")
+    for tag, N, L in (("N256_L128", 256, 128), ("N256_L256", 256, 256), ("N1024_L128", 1024, 128)):
+        assert _bad(oracle.scl_decode(N, L, d[tag + "_frozen"], d[tag + "_llr"], threads=8), d[tag + "_scl"]) == 0
+
+
 def test_numpy_restatement_pinned():
     """oracle/refnumpy.py (the CPU baseline bench.py times as "the reference's
     NumPy path") reproduces the reference's outputs: SC / SCL on the config-1

@@ -48,6 +48,9 @@ namespace {
 #ifndef RANK_STRICT_LCAP
 #define RANK_STRICT_LCAP 8  // list capacities ranked with strict comparisons
 #endif
+#ifndef PL_RANK_F32
+#define PL_RANK_F32 1  // strict ranks from fp32 roundings of the metrics (collisions fall back)
+#endif
 
 constexpr int RB = 5;  // bits per slot field of a pointer row (list capacity <= 32)
 
@@ -462,7 +465,10 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 double m0, m1;
                 path_metrics_fast<true>(pm, lam, slot < nact, m0, m1);
                 STAMP(3);
-                met[slot] = make_double2(m0, m1);
+                constexpr bool STRICT = LCAP >= RANK_STRICT_LCAP || NL >= 11;
+                constexpr bool F32 = STRICT && PL_RANK_F32;
+                if constexpr (F32) reinterpret_cast<float2*>(met)[slot] = make_float2((float)m0, (float)m1);
+                else met[slot] = make_double2(m0, m1);
                 rowx[2 * slot] = lrow;
                 rowx[2 * slot + 1] = brow;
                 brx[slot] = (uint64_t)bb | ((uint64_t)bw5 << 32);
@@ -492,7 +498,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 const int nsurv = (2 * nact < Lsz) ? 2 * nact : Lsz;
                 const uint32_t id0 = (uint32_t)(slot << 1), id1 = id0 | 1u;
                 int r0, r1;
-                if constexpr (LCAP >= RANK_STRICT_LCAP || NL >= 11) {
+                if constexpr (STRICT) {
                     // Lists of 8+ / long codes: strict comparisons only -- exact unless two
                     // candidates tie (inactive slots publish -inf and never
                     // count).  A tie makes two candidates claim one survivor
@@ -500,17 +506,38 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     // the stable tie-break.  (L = 32: 9.1 -> 7.5 ms, L = 16:
                     // 7.7 -> 7.0 ms, N = 2048 / 4096 L = 8: ~2 %, N = 1024 L = 8
                     // with shadow lanes: 6.72 -> 6.54 ms.)
+                    // F32: the comparisons use the fp32 roundings, half the LDS
+                    // bytes of the rank loop.  Rounding is monotone, so a > b in
+                    // fp32 implies a > b; two candidates that round equal get
+                    // the same rank and collide like a tie, and ranks at or past
+                    // the survivors cannot hide one below them.
                     r0 = 0;
                     r1 = 0;
-                    for (int q0 = 0; q0 < nact; q0 += QC) {
-                        double2 mq[QC];
+                    if constexpr (F32) {
+                        const float f0 = (float)m0, f1 = (float)m1;
+                        const float2* const met32 = reinterpret_cast<const float2*>(met);
+                        for (int q0 = 0; q0 < nact; q0 += QC) {
+                            float2 mq[QC];
 #pragma unroll
-                        for (int k = 0; k < QC; ++k) mq[k] = met[q0 + k];
+                            for (int k = 0; k < QC; ++k) mq[k] = met32[q0 + k];
 #pragma unroll
-                        for (int k = 0; k < QC; ++k) {
-                            const double a = mq[k].x, b = mq[k].y;
-                            r0 += (a > m0) + (b > m0);
-                            r1 += (a > m1) + (b > m1);
+                            for (int k = 0; k < QC; ++k) {
+                                const float a = mq[k].x, b = mq[k].y;
+                                r0 += (a > f0) + (b > f0);
+                                r1 += (a > f1) + (b > f1);
+                            }
+                        }
+                    } else {
+                        for (int q0 = 0; q0 < nact; q0 += QC) {
+                            double2 mq[QC];
+#pragma unroll
+                            for (int k = 0; k < QC; ++k) mq[k] = met[q0 + k];
+#pragma unroll
+                            for (int k = 0; k < QC; ++k) {
+                                const double a = mq[k].x, b = mq[k].y;
+                                r0 += (a > m0) + (b > m0);
+                                r1 += (a > m1) + (b > m1);
+                            }
                         }
                     }
                     if (slot < nact) {
@@ -518,9 +545,12 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                         if (r1 < nsurv) surv[r1] = id1;
                     }
                     lds_sync();
+                    // fp64 metrics over the fp32 copies (all read before the sync)
+                    if constexpr (F32) met[slot] = make_double2(m0, m1);
                     const bool lost =
                         slot < nact && ((r0 < nsurv && surv[r0] != id0) || (r1 < nsurv && surv[r1] != id1));
                     if (__ballot(lost)) {
+                        if constexpr (F32) lds_sync();  // the fp64 metrics of every lane
                         exact_ranks(r0, r1);
                         lds_sync();  // every lane has read surv before it is rewritten
                         if (slot < nact) {

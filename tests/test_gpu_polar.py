@@ -322,6 +322,30 @@ def test_large_list_ties_vs_oracle(gpu, oracle, L):
     assert _mismatch(out.cpu().numpy(), want) == 0
 
 
+@pytest.mark.parametrize("N,L", [(1024, 8), (1024, 16), (1024, 32), (4096, 8)])
+def test_near_tie_metrics_vs_oracle(gpu, oracle, N, L):
+    """Channel LLRs of (nearly) one magnitude, 5 +- 1e-7: competing path metrics
+    differ far below fp32 resolution, so the tree kernel's fp32 strict ranks
+    collide constantly and its exact fp64 fallback decides -- bits must match
+    the oracle."""
+    from polarcode_and_ldpc_amd import _native
+    P = _P()
+    K = N // 2
+    fr = P.construct_frozen_set(N, K, 2.0)
+    rng = np.random.RandomState(N + L)
+    B = 16
+    cw = P.PolarEncoder(N, K, frozen_bits=fr).encode_batch(rng.randint(0, 2, (B, K)))
+    sign = (1.0 - 2.0 * cw) * np.where(rng.rand(B, N) < 0.12, -1.0, 1.0)  # ~12 % flipped
+    llr = sign * (5.0 + 1e-7 * rng.rand(B, N))
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    plan = _native.polar_plan(N, K, mask, L)
+    assert plan.info.reserved == 4
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    plan.decode(torch.from_numpy(llr).cuda(), out)
+    assert _mismatch(out.cpu().numpy(), oracle.scl_decode(N, L, fr, llr, threads=8)) == 0
+
+
 def test_empty_batch(gpu):
     """A zero-frame batch decodes to an empty [0, K] result (SC, SCL tree and
     lane kernels) without launching."""

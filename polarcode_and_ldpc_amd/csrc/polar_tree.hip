@@ -52,6 +52,25 @@ namespace {
 #define PL_RANK_F32 1  // strict ranks from fp32 roundings of the metrics (collisions fall back)
 #endif
 
+// Lane exchanges inside the 8-lane group of a frame (LCAP = 8) without LDS:
+// quad_perm xor 1/2/3 and row_half_mirror (lane i <- 7 - i = i ^ 7 in each
+// half-row); xor 4/5/6 are a quad_perm of the mirrored value.
+template <int CTRL>
+PL_DEV int dpp_i(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false); }
+constexpr int DPP_X1 = 0xB1, DPP_X2 = 0x4E, DPP_X3 = 0x1B, DPP_MIRROR8 = 0x141;
+// fn(x of lane slot ^ k) for k = 1..7 of the lane's 8-lane group
+template <class Fn>
+PL_DEV void group8_each(int x, Fn fn) {
+    const int m = dpp_i<DPP_MIRROR8>(x);
+    fn(dpp_i<DPP_X1>(x));
+    fn(dpp_i<DPP_X2>(x));
+    fn(dpp_i<DPP_X3>(x));
+    fn(dpp_i<DPP_X3>(m));
+    fn(dpp_i<DPP_X2>(m));
+    fn(dpp_i<DPP_X1>(m));
+    fn(m);
+}
+
 constexpr int RB = 5;  // bits per slot field of a pointer row (list capacity <= 32)
 
 template <int NL, int LCAP_, int F_, int DL_>
@@ -467,12 +486,18 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 STAMP(3);
                 constexpr bool STRICT = LCAP >= RANK_STRICT_LCAP || NL >= 11;
                 constexpr bool F32 = STRICT && PL_RANK_F32;
-                if constexpr (F32) reinterpret_cast<float2*>(met)[slot] = make_float2((float)m0, (float)m1);
+                // DPP: the fp32 ranks from lane exchanges inside the frame's 8
+                // lanes instead of an LDS round trip (N=1024 6.42 -> 6.38 ms,
+                // N=4096 11.69 -> 11.51 ms).  Finding each survivor the same way
+                // (a search over the 8 lanes' ranks instead of the LDS survivor
+                // table) measured slower: 6.52 ms.
+                constexpr bool DPP = F32 && LCAP == 8;
+                if constexpr (F32 && !DPP) reinterpret_cast<float2*>(met)[slot] = make_float2((float)m0, (float)m1);
                 else met[slot] = make_double2(m0, m1);
                 rowx[2 * slot] = lrow;
                 rowx[2 * slot + 1] = brow;
                 brx[slot] = (uint64_t)bb | ((uint64_t)bw5 << 32);
-                lds_sync();
+                if constexpr (!DPP) lds_sync();
                 // rank of (slot, b) in the stable descending order of
                 // [(m0, q) for active q] + [(m1, q) for active q]
                 constexpr int QC = LCAP < 8 ? LCAP : 8;
@@ -497,13 +522,17 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 };
                 const int nsurv = (2 * nact < Lsz) ? 2 * nact : Lsz;
                 const uint32_t id0 = (uint32_t)(slot << 1), id1 = id0 | 1u;
+                // survivor this lane takes (decoder.py:323-336); lanes beyond the
+                // survivors shadow survivor 0 (see `plane`)
+                const int tgt = slot < nsurv ? slot : 0;
+                uint32_t e = 0;  // survivor entry: parent slot << 1 | bit
                 int r0, r1;
                 if constexpr (STRICT) {
                     // Lists of 8+ / long codes: strict comparisons only -- exact unless two
                     // candidates tie (inactive slots publish -inf and never
                     // count).  A tie makes two candidates claim one survivor
-                    // slot; the loser sees it and the wave redoes the ranks with
-                    // the stable tie-break.  (L = 32: 9.1 -> 7.5 ms, L = 16:
+                    // slot; the wave sees it and redoes the ranks with the
+                    // stable tie-break.  (L = 32: 9.1 -> 7.5 ms, L = 16:
                     // 7.7 -> 7.0 ms, N = 2048 / 4096 L = 8: ~2 %, N = 1024 L = 8
                     // with shadow lanes: 6.72 -> 6.54 ms.)
                     // F32: the comparisons use the fp32 roundings, half the LDS
@@ -513,7 +542,18 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     // the survivors cannot hide one below them.
                     r0 = 0;
                     r1 = 0;
-                    if constexpr (F32) {
+                    if constexpr (DPP) {
+                        const float f0 = (float)m0, f1 = (float)m1;
+                        r0 = f1 > f0;  // own pair (f0 > f0 never counts)
+                        r1 = f0 > f1;
+                        auto cmp = [&](int v) {
+                            const float c = __int_as_float(v);
+                            r0 += c > f0;
+                            r1 += c > f1;
+                        };
+                        group8_each(__float_as_int(f0), cmp);
+                        group8_each(__float_as_int(f1), cmp);
+                    } else if constexpr (F32) {
                         const float f0 = (float)m0, f1 = (float)m1;
                         const float2* const met32 = reinterpret_cast<const float2*>(met);
                         for (int q0 = 0; q0 < nact; q0 += QC) {
@@ -546,17 +586,20 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     }
                     lds_sync();
                     // fp64 metrics over the fp32 copies (all read before the sync)
-                    if constexpr (F32) met[slot] = make_double2(m0, m1);
+                    if constexpr (F32 && !DPP) met[slot] = make_double2(m0, m1);
+                    // a lost claim = a tie; the survivor entry is read in the same trip
                     const bool lost =
                         slot < nact && ((r0 < nsurv && surv[r0] != id0) || (r1 < nsurv && surv[r1] != id1));
+                    e = surv[tgt];
                     if (__ballot(lost)) {
-                        if constexpr (F32) lds_sync();  // the fp64 metrics of every lane
+                        lds_sync();  // the fp64 metrics of every lane; surv reads done
                         exact_ranks(r0, r1);
-                        lds_sync();  // every lane has read surv before it is rewritten
                         if (slot < nact) {
                             if (r0 < nsurv) surv[r0] = id0;
                             if (r1 < nsurv) surv[r1] = id1;
                         }
+                        lds_sync();
+                        e = surv[tgt];
                     }
                 } else {
                     exact_ranks(r0, r1);
@@ -564,12 +607,11 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                         if (r0 < nsurv) surv[r0] = id0;
                         if (r1 < nsurv) surv[r1] = id1;
                     }
+                    lds_sync();
+                    e = surv[tgt];
                 }
-                lds_sync();
+                lds_sync();  // met / rows of every lane written
                 if (G::SHADOW || slot < nsurv) {
-                    // survivor `slot` (decoder.py:323-336); lanes beyond the
-                    // survivors shadow survivor 0 (see `plane`) with metric -inf
-                    const uint32_t e = surv[slot < nsurv ? slot : 0];
                     const int par = (int)(e >> 1);
                     bit = (int)(e & 1u);
                     const double2 pmv = met[par];

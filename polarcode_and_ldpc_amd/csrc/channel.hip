@@ -232,19 +232,55 @@ hipError_t bsc_launch(const uint8_t* cw, int n, int64_t batch, double p, uint64_
     });
 }
 
-// one wavefront per frame; per-block partial sums -> 3 integer atomics
+// Bit / frame error counts of dec against ref (low bit of each byte), per-block
+// partial sums -> 3 integer atomics.  cpr = 16-byte chunks per row when both
+// row sets are 16-byte aligned with a width multiple of 16 (else 0: bytes):
+//   cpr a power of two <= 64: 64 / cpr rows per wavefront, one chunk per lane;
+//   otherwise: one row per wavefront, chunks (cpr > 0) or bytes strided by 64.
 __global__ void __launch_bounds__(256)
 count_errors_kernel(const uint8_t* __restrict__ ref, int64_t ldr, const uint8_t* __restrict__ dec,
-                    int64_t ldd, int width, int64_t batch, int64_t* counts) {
+                    int64_t ldd, int width, int64_t batch, int64_t* counts, int cpr) {
     __shared__ unsigned long long part[2][4];
     const int wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * 4, w0 = (int64_t)blockIdx.x * 4 + wave;
+    auto chunk_err = [&](int64_t b, int c) -> int {
+        const uint4 x = reinterpret_cast<const uint4*>(ref + b * ldr)[c];
+        const uint4 y = reinterpret_cast<const uint4*>(dec + b * ldd)[c];
+        constexpr uint32_t M = 0x01010101u;
+        return __popc((x.x ^ y.x) & M) + __popc((x.y ^ y.y) & M) + __popc((x.z ^ y.z) & M) +
+               __popc((x.w ^ y.w) & M);
+    };
     unsigned long long be = 0, fe = 0;
-    for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < batch; b += (int64_t)gridDim.x * 4) {
-        int e = 0;
-        for (int j = lane; j < width; j += 64) e += (ref[b * ldr + j] & 1) != (dec[b * ldd + j] & 1);
-        for (int s = 32; s > 0; s >>= 1) e += __shfl_xor(e, s);
-        be += (unsigned)e;
-        fe += e > 0 ? 1 : 0;
+    if (cpr > 0 && cpr <= 64 && (cpr & (cpr - 1)) == 0) {
+        const int rpw = 64 / cpr;
+        const int64_t r = lane / cpr;
+        for (int64_t b0 = w0 * rpw; b0 < batch; b0 += waves * rpw) {
+            const int64_t b = b0 + r;
+            int e = b < batch ? chunk_err(b, lane % cpr) : 0;
+            for (int sh = cpr / 2; sh > 0; sh >>= 1) e += __shfl_xor(e, sh);
+            if (lane % cpr == 0) {
+                be += (unsigned)e;
+                fe += e > 0 ? 1 : 0;
+            }
+        }
+    } else {
+        for (int64_t b = w0; b < batch; b += waves) {
+            int e = 0;
+            if (cpr > 0) {
+                for (int c = lane; c < cpr; c += 64) e += chunk_err(b, c);
+            } else {
+                for (int j = lane; j < width; j += 64) e += (ref[b * ldr + j] & 1) != (dec[b * ldd + j] & 1);
+            }
+            for (int sh = 32; sh > 0; sh >>= 1) e += __shfl_xor(e, sh);
+            if (lane == 0) {
+                be += (unsigned)e;
+                fe += e > 0 ? 1 : 0;
+            }
+        }
+    }
+    for (int sh = 32; sh > 0; sh >>= 1) {
+        be += __shfl_xor(be, sh);
+        fe += __shfl_xor(fe, sh);
     }
     if (lane == 0) { part[0][wave] = be; part[1][wave] = fe; }
     __syncthreads();
@@ -322,10 +358,14 @@ hipError_t crc_append_launch(uint8_t* msg, int64_t ld, int64_t batch, int k_data
 hipError_t count_errors_launch(const uint8_t* ref, int64_t ldr, const uint8_t* dec, int64_t ldd, int width,
                                int64_t batch, int64_t* counts, hipStream_t s) {
     if (batch == 0) return hipSuccess;
-    int64_t blocks = (batch + 3) / 4;
-    if (blocks > 4096) blocks = 4096;
+    const bool vec = width % 16 == 0 && ldr % 16 == 0 && ldd % 16 == 0 && ((uintptr_t)ref & 15) == 0 &&
+                     ((uintptr_t)dec & 15) == 0;
+    const int cpr = vec ? width / 16 : 0;
+    const int rpw = (cpr > 0 && cpr <= 64 && (cpr & (cpr - 1)) == 0) ? 64 / cpr : 1;  // rows per wavefront
+    int64_t blocks = (batch + 4 * rpw - 1) / (4 * rpw);
+    if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(count_errors_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ref, ldr, dec, ldd, width,
-                       batch, counts);
+                       batch, counts, cpr);
     return hipGetLastError();
 }
 

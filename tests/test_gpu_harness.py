@@ -114,3 +114,27 @@ def test_ldpc_mc_random_codewords_match_zero_codeword(gpu):
     _, lo_z, hi_z = wilson_interval(res["zero"].frame_errors, res["zero"].frames, 0.999)
     _, lo_r, hi_r = wilson_interval(res["random"].frame_errors, res["random"].frames, 0.999)
     assert lo_z <= hi_r and lo_r <= hi_z, (fz, fr)
+
+
+@pytest.mark.parametrize("width,ld,off", [(512, 512, 0), (512, 528, 16), (252, 252, 0), (504, 512, 0),
+                                          (16, 16, 0), (1024, 1024, 0), (2048, 2048, 0), (8192, 8192, 0),
+                                          (512, 512, 3), (7, 9, 1)])
+def test_count_errors_vs_torch(gpu, width, ld, off):
+    """pl_count_errors (16-byte chunk paths for aligned rows, byte path otherwise)
+    against a torch count of low-bit mismatches; rows with 0, 1 and many errors."""
+    from polarcode_and_ldpc_amd import _native
+    B = 3001
+    g = torch.Generator(device="cuda").manual_seed(width * 7 + off)
+    base_r = torch.randint(0, 256, (B * ld + off + 64,), dtype=torch.uint8, device="cuda", generator=g)
+    base_d = base_r.clone()
+    flip = torch.rand((B, width), device="cuda", generator=g) < torch.rand((B, 1), device="cuda", generator=g) ** 4
+    flip[::5] = False
+    ref = base_r[off:off + B * ld].view(B, ld)[:, :width]
+    dec = base_d[off:off + B * ld].view(B, ld)[:, :width]
+    dec ^= flip.to(torch.uint8) | (torch.randint(0, 128, (B, width), dtype=torch.uint8, device="cuda",
+                                                 generator=g) << 1)
+    counts = torch.zeros(3, dtype=torch.int64, device="cuda")
+    _native.count_errors(ref, dec, width, counts)
+    e = ((ref & 1) != (dec & 1)).sum(dim=1)
+    want = [int(e.sum()), int((e > 0).sum()), B]
+    assert counts.tolist() == want

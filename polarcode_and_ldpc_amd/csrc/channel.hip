@@ -363,7 +363,7 @@ hipError_t count_errors_launch(const uint8_t* ref, int64_t ldr, const uint8_t* d
     const int cpr = vec ? width / 16 : 0;
     const int rpw = (cpr > 0 && cpr <= 64 && (cpr & (cpr - 1)) == 0) ? 64 / cpr : 1;  // rows per wavefront
     int64_t blocks = (batch + 4 * rpw - 1) / (4 * rpw);
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(count_errors_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ref, ldr, dec, ldd, width,
                        batch, counts, cpr);
     return hipGetLastError();

@@ -247,9 +247,9 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
         if (regular && maxdv < 8 && E < 65536) g.reg_variant = pl::ldpc_reg_variant(maxdv, E, n);
         if (g.reg_variant) {
             g.threads = 256;
-            // + the BP tanh work list: E 16-bit indices + a counter (ldpc_reg_kernel)
+            // + the per-wavefront BP tanh lists (ldpc_reg_kernel)
             const size_t base = ((size_t)2 * E * 8 + lds_small + 15) & ~(size_t)15;
-            g.lds_bytes = (int)((base + (((size_t)2 * E + 3) & ~(size_t)3) + 16 + 15) & ~(size_t)15);
+            g.lds_bytes = (int)((base + pl::ldpc_reg_list_bytes(g.reg_variant) + 15) & ~(size_t)15);
         }
     }
     // min-sum codes whose T/C arrays exceed LDS: compressed check state in LDS

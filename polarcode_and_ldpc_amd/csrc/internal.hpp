@@ -94,5 +94,6 @@ hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, i
 hipError_t ldpc_prepare(const LdpcGeom& g);
 size_t ldpc_work_bytes_per_frame(const LdpcGeom& g);
 int ldpc_reg_variant(int dv, int E, int n);  // 0: none fits
+size_t ldpc_reg_list_bytes(int variant);      // BP tanh lists of an ldpc_reg_kernel instance
 
 }  // namespace pl

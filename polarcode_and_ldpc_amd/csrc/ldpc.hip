@@ -259,12 +259,12 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
     double* C = T + E;
     uint32_t* syn = reinterpret_cast<uint32_t*>(smem + (size_t)16 * E);  // [2][m]
     uint8_t* bt = reinterpret_cast<uint8_t*>(syn + 2 * m);               // [n]
-    // BP: edges whose v2c needs a tanh (|x| <= 14.52 or NaN), compacted: [E]
-    // 16-bit edge indices (E < 65536) + a counter; 29 KB per frame at (504,252),
-    // so 5 frames fit a CU's LDS (capi.cpp sizes it)
+    // BP: per-wavefront lists of the edges whose v2c needs a tanh (|x| <= 14.52
+    // or NaN), 16-bit edge indices (E < 65536), 64*VPT*DV per wavefront: each
+    // wavefront compacts and evaluates its own, so the tanh pass needs no
+    // workgroup barrier.  29 KB per frame at (504,252), so 5 frames fit a CU's
+    // LDS (capi.cpp sizes it with ldpc_reg_list_bytes)
     uint16_t* work = reinterpret_cast<uint16_t*>(smem + (((size_t)16 * E + (size_t)8 * m + n + 15) & ~(size_t)15));
-    int32_t* wcnt = reinterpret_cast<int32_t*>(smem + ((((size_t)16 * E + (size_t)8 * m + n + 15) & ~(size_t)15) +
-                                                       (((size_t)2 * E + 3) & ~(size_t)3)));
     const double* __restrict__ ch = llr + frame * ld;
     auto tin = [&](double x) -> double { return ALGO == 0 ? tanh_half_clip(x) : x; };
     const int lane = __lane_id();
@@ -289,7 +289,6 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         chv[j] = ok ? ch[v] : 0.0;
     }
     for (int c = tid; c < 2 * m; c += NT) syn[c] = 0u;
-    if (tid == 0) *wcnt = 0;
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
         if (tid + j * NT < n) {
@@ -350,10 +349,13 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
             C[e] = o;
         }
         __syncthreads();
+        uint16_t* const wl = work + (tid >> 6) * (64 * VPT * DV);  // this wavefront's tanh list
+        int wn = 0;                                                 // its length (wavefront-uniform)
 #pragma unroll
         for (int j = 0; j < VPT; ++j) {
             const int v = tid + j * NT;
-            if (v >= n) break;
+            const bool vok = v < n;  // lanes past n run along (ve = 0) with every store masked
+            if (!__ballot(vok)) break;
             double c2v[DV];
             double sum = 0.0;  // np.sum over DV < 8 messages: sequential
 #pragma unroll
@@ -363,44 +365,38 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
             }
             const double total = chv[j] + sum;
             const bool one = total <= 0.0;
-            bt[v] = one ? 1 : 0;
+            if (vok) bt[v] = one ? 1 : 0;
 #pragma unroll
             for (int k = 0; k < DV; ++k) {
                 const double x = total - c2v[k];  // v2c as decoder.py:120 forms it
                 if (ALGO == 0) {
                     // saturated inputs take the clip value now; the rest are
-                    // appended to the work list and get their tanh below, in a
-                    // dense pass over all of the frame's threads
+                    // appended to the wavefront's list and get their tanh below
                     const bool sat = fabs(x) > 14.52;
-                    T[ve[j][k]] = sat ? __builtin_copysign(0.999999, x) : x;
-                    const uint64_t need = __ballot(!sat);
-                    if (need) {
-                        const uint64_t act = __ballot(1);
-                        const int leader = __ffsll((unsigned long long)act) - 1;
-                        int base = 0;
-                        if (lane == leader) base = atomicAdd(wcnt, (int)__popcll(need));
-                        base = __builtin_amdgcn_readlane(base, leader);
-                        const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                        if (!sat) work[base + pre] = (uint16_t)ve[j][k];
-                    }
-                } else {
+                    if (vok) T[ve[j][k]] = sat ? __builtin_copysign(0.999999, x) : x;
+                    const bool need = vok && !sat;
+                    const uint64_t nb = __ballot(need);
+                    const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nb >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)nb, 0u));
+                    if (need) wl[wn + pre] = (uint16_t)ve[j][k];
+                    wn += (int)__popcll(nb);
+                } else if (vok) {
                     T[ve[j][k]] = x;
                 }
-                if (one) atomicXor(&scur[vc[j][k]], 1u);
+                if (vok && one) atomicXor(&scur[vc[j][k]], 1u);
             }
         }
         if (ALGO == 0) {
-            __syncthreads();
-            const int nw = *wcnt;
-            for (int w = tid; w < nw; w += NT) {
-                const int e = work[w];
+            // the list and its T entries were written by this wavefront, and LDS
+            // runs a wavefront's operations in order: no barrier
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            for (int w = lane; w < wn; w += 64) {
+                const int e = wl[w];
                 T[e] = tanh_half_clip(T[e]);
             }
-            __syncthreads();
-            if (tid == 0) *wcnt = 0;  // read by every thread before the barrier above
         }
-        __syncthreads();
+        __syncthreads();  // T and the syndrome parities for the next iteration's vote / check pass
     }
     uint8_t* o = bits + frame * (int64_t)n;
     for (int v = tid; v < n; v += NT) o[v] = bt[v];
@@ -418,6 +414,11 @@ static const RegVariant* reg_table(int& count) {
                                    reg_variant<3, 16, 4>(), reg_variant<4, 8, 2>(), reg_variant<4, 16, 4>()};
     count = (int)(sizeof(t) / sizeof(t[0]));
     return t;
+}
+size_t ldpc_reg_list_bytes(int variant) {
+    int cnt;
+    const RegVariant* t = reg_table(cnt);
+    return variant > 0 && variant <= cnt ? (size_t)256 * t[variant - 1].vpt * t[variant - 1].dv * 2 : 0;
 }
 int ldpc_reg_variant(int dv, int E, int n) {
     int cnt;

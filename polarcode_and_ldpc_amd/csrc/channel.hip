@@ -254,13 +254,18 @@ count_errors_kernel(const uint8_t* __restrict__ ref, int64_t ldr, const uint8_t*
     if (cpr > 0 && cpr <= 64 && (cpr & (cpr - 1)) == 0) {
         const int rpw = 64 / cpr;
         const int64_t r = lane / cpr;
-        for (int64_t b0 = w0 * rpw; b0 < batch; b0 += waves * rpw) {
-            const int64_t b = b0 + r;
+        // two row groups per trip: their loads are in flight together
+        for (int64_t b0 = w0 * rpw; b0 < batch; b0 += 2 * waves * rpw) {
+            const int64_t b = b0 + r, b2 = b + waves * rpw;
             int e = b < batch ? chunk_err(b, lane % cpr) : 0;
-            for (int sh = cpr / 2; sh > 0; sh >>= 1) e += __shfl_xor(e, sh);
+            int e2 = b2 < batch ? chunk_err(b2, lane % cpr) : 0;
+            for (int sh = cpr / 2; sh > 0; sh >>= 1) {
+                e += __shfl_xor(e, sh);
+                e2 += __shfl_xor(e2, sh);
+            }
             if (lane % cpr == 0) {
-                be += (unsigned)e;
-                fe += e > 0 ? 1 : 0;
+                be += (unsigned)(e + e2);
+                fe += (e > 0 ? 1 : 0) + (e2 > 0 ? 1 : 0);
             }
         }
     } else {
@@ -362,8 +367,8 @@ hipError_t count_errors_launch(const uint8_t* ref, int64_t ldr, const uint8_t* d
                      ((uintptr_t)dec & 15) == 0;
     const int cpr = vec ? width / 16 : 0;
     const int rpw = (cpr > 0 && cpr <= 64 && (cpr & (cpr - 1)) == 0) ? 64 / cpr : 1;  // rows per wavefront
-    int64_t blocks = (batch + 4 * rpw - 1) / (4 * rpw);
-    if (blocks > 8192) blocks = 8192;
+    int64_t blocks = (batch + 8 * rpw - 1) / (8 * rpw);
+    if (blocks > 512) blocks = 512;  // two same-address atomics per block: keep them few
     hipLaunchKernelGGL(count_errors_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ref, ldr, dec, ldd, width,
                        batch, counts, cpr);
     return hipGetLastError();

@@ -48,6 +48,9 @@ namespace {
 #ifndef RANK_STRICT_LCAP
 #define RANK_STRICT_LCAP 8  // list capacities ranked with strict comparisons
 #endif
+#ifndef PL_RATE0
+#define PL_RATE0 2  // rate-0 nodes of 2..8 leaves decoded at their first leaf; >= 2: metric chains per group
+#endif
 #ifndef PL_RANK_F32
 #define PL_RANK_F32 1  // strict ranks from fp32 roundings of the metrics (collisions fall back)
 #endif
@@ -352,6 +355,85 @@ PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, in
     return fused_loop<G, 0>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw);
 }
 
+// Size 2^k (k <= 3) of the rate-0 node (all leaves frozen) whose first leaf is
+// decode-order leaf i, 0 if none: i a multiple of 2^k, leaves i .. i+2^k-1
+// frozen (one mask word holds them).
+PL_DEV int rate0_k(const uint32_t* __restrict__ frozen_dec, int i) {
+    const uint32_t w = frozen_dec[i >> 5] >> (i & 31);
+    return ((i & 7) == 0 && (w & 0xFFu) == 0xFFu)  ? 3
+           : ((i & 3) == 0 && (w & 0xFu) == 0xFu) ? 2
+           : ((i & 1) == 0 && (w & 3u) == 3u)     ? 1
+                                                  : 0;
+}
+
+// Leaf LLRs of a rate-0 node (every leaf frozen, so every partial sum inside
+// it is 0 and the g of a right child is btm + top): the leaves of A are the
+// leaves of its f-child, then those of its g-child -- the very f / g the leaf
+// by leaf schedule evaluates on the same operands.
+template <int S>
+PL_DEV void rate0_leaves(const double* A, double* out) {
+    if constexpr (S == 1) {
+        out[0] = A[0];
+    } else {
+        double L[S / 2], R[S / 2];
+#pragma unroll
+        for (int t = 0; t < S / 2; ++t) {
+            L[t] = f_ms(A[2 * t], A[2 * t + 1]);
+            R[t] = g_op(A[2 * t], A[2 * t + 1], 0u);
+        }
+        rate0_leaves<S / 2>(L, out);
+        rate0_leaves<S / 2>(R, out + S / 2);
+    }
+}
+
+// Leaves i+1 .. i+2^K-1 of the rate-0 node at depth n-K whose first leaf i was
+// just decoded: its LLR array is the depth-(n-K) pool the descent to leaf i
+// stored (this lane's plane); their path-metric increments (bit 0) are added
+// in leaf order.  SC: nothing to evaluate.
+template <class G, int K, bool SC>
+PL_DEV void rate0_rest(const unsigned char* smem, const unsigned char* ws, int plane, bool active, double& pm) {
+    if constexpr (!SC) {
+        constexpr int S = 1 << K, D = G::n - K;
+        const double2* src = reinterpret_cast<const double2*>((D >= G::DL ? smem : ws) + G::llr_off(D)) + plane;
+        double a[S], ll[S];
+#pragma unroll
+        for (int j = 0; j < S / 2; ++j) {
+            const double2 pr = src[j * 64];
+            a[2 * j] = pr.x;
+            a[2 * j + 1] = pr.y;
+        }
+        rate0_leaves<S>(a, ll);
+#if PL_RATE0 >= 2
+        // increments of PL_RATE0 leaves evaluated together (independent chains),
+        // always computed: where path_metrics_fast skips t it is below a quarter
+        // ulp of every addend and the sums are the same
+        constexpr int IL = PL_RATE0;
+#pragma unroll
+        for (int j0 = 1; j0 < S; j0 += IL) {
+            double inc[IL];
+#pragma unroll
+            for (int u = 0; u < IL; ++u) {
+                if (j0 + u < S) {
+                    const double lam = ll[j0 + u];
+                    const double t = log1p_pos(exp_neg(fabs(lam)));
+                    inc[u] = (lam >= 0.0) ? -t : lam - t;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < IL; ++u)
+                if (j0 + u < S && active) pm = pm + inc[u];
+        }
+#else
+#pragma unroll
+        for (int j = 1; j < S; ++j) {
+            double m0, m1;
+            path_metrics_fast<false>(pm, ll[j], active, m0, m1);
+            if (active) pm = m0;
+        }
+#endif
+    }
+}
+
 template <class G, int P>
 PL_DEV double descend_from(int p, unsigned char* smem, unsigned char* ws, int plane, int ps, int bs, uint32_t bb,
                            uint32_t bw5) {
@@ -628,6 +710,31 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 nact = nsurv;
                 lds_sync();  // scratch reads done before the next leaf's writes
                 STAMP(4);
+            }
+
+            // ========================================= rate-0 node from leaf i
+            // Leaves i .. i+2^k-1 all frozen (k <= 3, i a multiple of 2^k): their
+            // bits are 0, so every partial sum inside the node is 0 and nothing
+            // the later leaves' descents, walks or pointer rows would produce
+            // is read after the node except the zeros walked up from its last
+            // leaf.  Their LLRs follow from the node's array (depth n-k, stored by
+            // the descent to leaf i) without a descent each; the metrics are
+            // added in leaf order.  Same operations on the same operands as the
+            // leaf-by-leaf schedule.
+            if constexpr (PL_RATE0 != 0) {
+                if (frozen) {
+                    const int k = rate0_k(frozen_dec, i);
+                    if (k > 0) {
+                        const int pslot = (!G::SHADOW || slot < nact) ? slot : 0;
+                        const int plane = G::pl(pslot, fw);
+                        if (k == 3) rate0_rest<G, 3, SC>(smem, ws, plane, slot < nact, pm);
+                        else if (k == 2) rate0_rest<G, 2, SC>(smem, ws, plane, slot < nact, pm);
+                        else rate0_rest<G, 1, SC>(smem, ws, plane, slot < nact, pm);
+                        bb &= ~((1u << ((1 << k) - 1)) - 1u);  // partial sums of depths n-k+1..n: 0
+                        i += (1 << k) - 1;                     // the walk below runs for the node's last leaf
+                        STAMP(3);
+                    }
+                }
             }
 
             // ================================================ partial-sum walk

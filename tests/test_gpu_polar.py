@@ -640,3 +640,28 @@ def test_scl_large_lists_golden_and_oracle(gpu, oracle):
     assert _mismatch(P.SCLDecoder(64, 32, list_size=256, frozen_bits=fr64).decode_batch(llr64), want) == 0
     with pytest.raises(ValueError):  # PL_EUNSUPPORTED: 8-bit path slots
         P.SCLDecoder(N, K, list_size=257, frozen_bits=fr).decode_batch(llr)
+
+
+@pytest.mark.parametrize("N,L,K", [(1024, 0, 300), (1024, 8, 512), (1024, 8, 40), (1024, 32, 700), (4096, 8, 2048),
+                                   (256, 4, 128), (128, 32, 16), (2048, 8, 1500), (512, 16, 256), (1024, 8, 1016)])
+def test_random_frozen_sets_rate0_nodes(gpu, oracle, N, L, K):
+    """Random frozen sets (every alignment and size of all-frozen runs in decode
+    order, so the tree kernel's rate-0 node path meets pairs / quads / octets
+    everywhere, next to long info runs) at low SNR: HIP vs the C oracle."""
+    P = _P()
+    rng = np.random.RandomState(N + 7 * L + K)
+    fr = np.sort(rng.choice(N, N - K, replace=False))
+    enc = P.PolarEncoder(N, K, frozen_bits=fr)
+    B = 32 if N * max(L, 1) <= 8192 else 12
+    msg = rng.randint(0, 2, (B, K))
+    cw = enc.encode_batch(msg)
+    snr = rng.uniform(-2.0, 2.0, size=(B, 1))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+    llr = 2.0 * ((1.0 - 2.0 * cw) + sigma * rng.randn(B, N)) / sigma ** 2
+    if L == 0:
+        want = oracle.sc_decode(N, fr, llr, threads=8)
+        got = P.SCDecoder(N, K, frozen_bits=fr).decode_batch(llr)
+    else:
+        want = oracle.scl_decode(N, L, fr, llr, threads=8)
+        got = P.SCLDecoder(N, K, list_size=L, frozen_bits=fr).decode_batch(llr)
+    assert _mismatch(got, want) == 0

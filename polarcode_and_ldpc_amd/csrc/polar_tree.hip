@@ -29,9 +29,14 @@
 //   * partial sums (beta) of depths n-5..n live in two registers per lane, the
 //     multi-word depths 1..n-6 in the workspace behind 5-bit slot pointers, as
 //     the LLR pools.  A list clone copies 24 bytes (rows + beta registers);
-//   * pruning runs through LDS: lanes publish (m0, m1) and rows, read their
-//     frame's metrics with 16-byte broadcasts (group stride padded against bank
-//     conflicts), rank, and scatter survivors to a slot table;
+//   * pruning: strict ranks from fp32 roundings of the metrics (ties and fp32
+//     collisions detected and redone exactly), read through DPP lane exchanges
+//     at LCAP 8 and from LDS with 16-byte broadcasts otherwise; survivors are
+//     scattered to an LDS slot table and take their parent's rows, partial-sum
+//     registers and metric from LDS;
+//   * rate-0 nodes of 2..8 leaves (all frozen) are decoded at their first leaf:
+//     the other leaves' LLRs from the node's stored array (beta = 0), their
+//     metric increments added in leaf order;
 //   * lane columns are slot-major and, while the list grows, lanes beyond the
 //     active paths shadow slot 0 (TG::SHADOW), so inactive paths cost no memory
 //     traffic.

@@ -47,7 +47,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 CLOCK_GHZ = 2.4
 
 
-SECTIONS = ("polar", "e2e", "polar_default", "ldpc", "ldpc_valid", "cascl", "sweep", "long_polar", "long_ms", "long_ms_noes")
+SECTIONS = ("polar", "e2e", "polar_default", "sc_default", "config0", "ldpc", "ldpc_valid", "cascl", "sweep",
+            "long_polar", "long_ms", "long_ms_noes")
 
 
 def log(*a):
@@ -184,6 +185,9 @@ def roofline(name, kernel, frames, bytes_per_frame, kms):
     r["traffic_source"] = p.get("source")
     r["traffic_GBps"] = r["traffic"] / (kms / 1e3) / 1e9
     r["traffic_frac"] = r["traffic_GBps"] / HBM_PEAK_GBS
+    r["traffic_frames_profiled"] = p.get("frames")
+    if "wave_time_shares" in p:
+        r["wave_time_shares"] = p["wave_time_shares"]
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     if "valu_fp64_per_launch" in p and "valu_per_launch" in p:
         scale = frames / float(p.get("frames", frames))
@@ -200,20 +204,64 @@ def roofline(name, kernel, frames, bytes_per_frame, kms):
 
 
 # ---------------------------------------------------------------- CPU baseline
+def cpu_share():
+    """(processes the CPU legs use, what the host offers).  The GPU box gives one
+    GPU a 16-CPU share of a larger host (os.sched_getaffinity lists every CPU of
+    the machine); the legs use min(affinity, cgroup quota, PL_BENCH_CPU_CAP=16)
+    processes and report the host's figures beside it."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except Exception:
+        pass
+    cap = int(os.environ.get("PL_BENCH_CPU_CAP", "16"))
+    used = max(1, min(aff, quota or aff, cap))
+    return used, dict(host_cpus_affinity=aff, cgroup_cpu_quota=quota, cap=cap, os_cpu_count=os.cpu_count())
+
+
 def cpu_processes():
-    return max(1, min(16, len(os.sched_getaffinity(0))))
+    return cpu_share()[0]
 
 
-def numpy_baseline(pool, procs, what, fn, frames, info_bits, gpu_bits):
-    """Time the NumPy restatement of the reference loops on `frames` frames."""
+def _mism(bits, gpu_bits):
+    return int((np.asarray(bits) != np.asarray(gpu_bits)).any(axis=1).sum())
+
+
+def numpy_baseline(pool, procs, what, fn, frames, info_bits, gpu_bits, single=None):
+    """Time the NumPy restatement of the reference loops on `frames` frames over
+    the pool; `single` = (fn, frames) times it in this process (one core)."""
     t0 = time.perf_counter()
     bits = fn()
     ct = time.perf_counter() - t0
-    return dict(value=frames * info_bits / ct / 1e6, unit="info-Mbps", cores=procs, kind="port",
-                sample="first %d frames of the same LLR batch: %s (oracle/refnumpy.py, the reference's NumPy "
-                       "per-frame loops restated, bit-exact with its fixtures), %d spawn processes, %.1f s"
-                       % (frames, what, procs, ct),
-                mismatching_frames_vs_gpu=int((bits != gpu_bits).any(axis=1).sum()))
+    res = dict(value=frames * info_bits / ct / 1e6, unit="info-Mbps", cores=procs, kind="port",
+               sample="first %d frames of the same LLR batch: %s (oracle/refnumpy.py, the reference's NumPy "
+                      "per-frame loops restated, bit-exact with its fixtures), %d spawn processes, %.1f s"
+                      % (frames, what, procs, ct),
+               mismatching_frames_vs_gpu=_mism(bits, gpu_bits), host=cpu_share()[1])
+    if single is not None:
+        sfn, sframes = single
+        t0 = time.perf_counter()
+        sb = sfn()
+        st = time.perf_counter() - t0
+        res["single_core"] = dict(value=sframes * info_bits / st / 1e6, unit="info-Mbps", cores=1, kind="port",
+                                  sample="first %d frames, one process, %.1f s" % (sframes, st),
+                                  mismatching_frames_vs_gpu=_mism(sb, gpu_bits[:sframes]))
+    return res
+
+
+def c_port(res, what, fn, frames, info_bits, gpu_bits, procs):
+    """The C restatement (oracle/refcpu.c, OpenMP) beside the NumPy figure."""
+    t0 = time.perf_counter()
+    bits = fn()
+    ct = time.perf_counter() - t0
+    res["c_port"] = dict(value=frames * info_bits / ct / 1e6, unit="info-Mbps", cores=procs, kind="port",
+                         sample="first %d frames, oracle/refcpu.c %s (loop-faithful C restatement), OpenMP %d "
+                                "threads, %.1f s" % (frames, what, procs, ct),
+                         mismatching_frames_vs_gpu=_mism(bits, gpu_bits))
+    return res
 
 
 # ---------------------------------------------------------------- polar
@@ -234,6 +282,13 @@ def polar_fixture(rt, N, K, L, B, snr, seed, frozen_snr=2.0):
     llr = AWGNChannel(snr).llr_batch_device(cw, N, B, seed=seed, frame_offset=off)
     del cw
     return dec, frozen, msg, llr
+
+
+def rank_fields(dt_per_rank, steps, counts):
+    """Per-rank step times (the value is taken at the max) and the counters
+    all-reduced over the ranks (frames counted = world x frames per GPU x steps)."""
+    return dict(rank_ms_per_step=[t / steps * 1e3 for t in dt_per_rank], frames_counted=int(counts[2]),
+                frame_errors=int(counts[1]), bit_errors=int(counts[0]))
 
 
 def polar_kernel_name(plan, n):
@@ -269,10 +324,10 @@ def decode_loop(rt, plan, llr, out, msg, width, steps, warmup, iters=None):
     return dt, per_rank, kt.mean_ms(), counts.cpu().numpy()
 
 
-def bench_polar(args, rt, pool):
+def _bench_headline(args, rt, pool, N, K, L, B):
+    """BASELINE configs[1] decode (+ the end-to-end Monte-Carlo step)."""
     from polarcode_and_ldpc_amd import _native
     from polarcode_and_ldpc_amd.channel import AWGNChannel
-    N, K, L, B = 1024, 512, args.list_size, args.batch
     dec, frozen, msg, llr = polar_fixture(rt, N, K, L, B, args.snr, 42)
     plan = dec.plan
     out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
@@ -282,6 +337,19 @@ def bench_polar(args, rt, pool):
                roofline=roofline("polar_scl_1024_l8", polar_kernel_name(plan, 10), B, 8 * N + K, kms),
                plan=dict(lds_bytes=plan.info.lds_bytes, fused_top=plan.info.fused_top),
                ber=float(c[0]) / max(1, c[2] * K), fer=float(c[1]) / max(1, c[2]), frames_counted=int(c[2]))
+    if pool is not None:
+        from oracle import oracle as O
+        from oracle import refnumpy as R
+        S, S1, S2 = args.cpu_frames_numpy, 8, args.cpu_frames
+        llr_h = llr[:max(S, S2)].cpu().numpy()
+        got = out[:llr_h.shape[0]].cpu().numpy().astype(np.int64)
+        procs = cpu_processes()
+        res["cpu_baseline"] = numpy_baseline(
+            pool, procs, "SCL N=1024 L=%d" % L, lambda: R.polar_batch(N, L, frozen, llr_h[:S], pool=pool), S, K,
+            got[:S], single=(lambda: R.polar_batch(N, L, frozen, llr_h[:S1]), S1))
+        c_port(res["cpu_baseline"], "SCL L=%d" % L, lambda: O.scl_decode(N, L, frozen, llr_h[:S2], threads=procs),
+               S2, K, got[:S2], procs)
+        del llr_h
 
     if "e2e" in args.sec:
         # End-to-end Monte Carlo (SURVEY §8 d): fresh messages, encoding, AWGN,
@@ -314,41 +382,149 @@ def bench_polar(args, rt, pool):
                                       "SCL decode + error count (+ all-reduce)",
                                  ber=float(e[0]) / max(1, e[2] * K), fer=float(e[1]) / max(1, e[2]))
         del msg2, out2, cw2, llr2
+        if pool is not None:
+            res["end_to_end"]["cpu_baseline"] = e2e_cpu_baseline(args, pool, dec, frozen, N, K, L)
+    return res
 
+
+def bench_polar(args, rt, pool):
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    N, K, L, B = 1024, 512, args.list_size, args.batch
+    res = {}
+    if "polar" in args.sec:
+        res.update(_bench_headline(args, rt, pool, N, K, L, B))
     if "polar_default" in args.sec:
         # like-for-like with throughput_test.py (SURVEY §8 d): the default frozen
         # set, info = indices whose bit reversal is >= N - K
-        dd, _, dmsg, dllr = polar_fixture(rt, N, K, L, B, args.snr, 47, frozen_snr=None)
+        dd, dfr, dmsg, dllr = polar_fixture(rt, N, K, L, B, args.snr, 47, frozen_snr=None)
         dout = torch.empty((B, K), dtype=torch.uint8, device="cuda")
-        ddt, _, dkms, dc = decode_loop(rt, dd.plan, dllr, dout, dmsg, K, args.steps, args.warmup)
+        ddt, dpr, dkms, dc = decode_loop(rt, dd.plan, dllr, dout, dmsg, K, args.steps, args.warmup)
         res["default_frozen_set"] = dict(
             metric="decoded info-Mbps, polar N=1024 K=512 SCL L=%d, reference default frozen set "
                    "(generate_frozen_bits) @ %.1f dB" % (L, args.snr),
             value=B * rt.world * args.steps * K / ddt / 1e6, unit="info-Mbps", ms_per_step=ddt / args.steps * 1e3,
-            kernel_ms=dkms, fer=float(dc[1]) / max(1, dc[2]),
+            kernel_ms=dkms, fer=float(dc[1]) / max(1, dc[2]), **rank_fields(dpr, args.steps, dc),
             roofline=roofline("polar_scl_1024_l8_default", polar_kernel_name(dd.plan, 10), B, 8 * N + K, dkms))
+        if pool is not None:
+            from oracle import refnumpy as R
+            S = args.cpu_frames_numpy
+            lh = dllr[:S].cpu().numpy()
+            res["default_frozen_set"]["cpu_baseline"] = numpy_baseline(
+                pool, cpu_processes(), "SCL N=1024 L=%d, default frozen set" % L,
+                lambda: R.polar_batch(N, L, dfr, lh, pool=pool), S, K, dout[:S].cpu().numpy().astype(np.int64))
         del dd, dmsg, dllr, dout
         torch.cuda.empty_cache()
+    return res
 
+
+def e2e_cpu_baseline(args, pool, dec, frozen, N, K, L):
+    """The reference's own frame loop (benchmarks/ber_simulation.py:167-189:
+    np.random.randint messages, host encoder, AWGNChannel.transmit, decode)
+    with the NumPy decode restatement, on S frames; the GPU decodes the same
+    host LLRs for the mismatch count."""
+    from oracle import refnumpy as R
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.polar import PolarEncoder
+    S = max(16, args.cpu_frames_numpy // 4)
+    state = np.random.get_state()
+    enc = PolarEncoder(N, K, frozen_bits=frozen)
+    ch = AWGNChannel(args.snr, seed=43)
+    t0 = time.perf_counter()
+    msgs = np.random.randint(0, 2, (S, K))
+    llr_h = ch.transmit(enc.encode_batch(msgs), return_llr=True)
+    bits = R.polar_batch(N, L, frozen, llr_h, pool=pool)
+    ct = time.perf_counter() - t0
+    np.random.set_state(state)
+    got = dec.decode_batch(torch.from_numpy(llr_h).cuda()).cpu().numpy().astype(np.int64)
+    procs = cpu_processes()
+    return dict(value=S * K / ct / 1e6, unit="info-Mbps", cores=procs, kind="port",
+                sample="%d frames of the reference's frame loop (messages, host encoder, AWGNChannel.transmit, "
+                       "NumPy SCL L=%d restatement), %d spawn processes, %.1f s" % (S, L, procs, ct),
+                mismatching_frames_vs_gpu=_mism(bits, got), host=cpu_share()[1])
+
+
+def bench_sc_default(args, rt, pool):
+    """The reference's published polar number (benchmarks/results/data/
+    throughput_results.json:4-14, produced by throughput_test.py:197-235): SC
+    N=1024 K=512, default frozen set (generate_frozen_bits), 3 dB."""
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.polar import SCDecoder
+    N, K, B = 1024, 512, args.batch
+    dec = SCDecoder(N, K)  # frozen_bits=None: the reference's default set
+    off = rt.rank * B
+    msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    _native.random_bits(48, off, msg)
+    cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+    _native.polar_encode(dec.plan, msg, cw)
+    llr = AWGNChannel(args.snr).llr_batch_device(cw, N, B, seed=48, frame_offset=off)
+    del cw
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    dt, pr, kms, c = decode_loop(rt, dec.plan, llr, out, msg, K, args.steps, args.warmup)
+    res = dict(metric="decoded info-Mbps, polar N=1024 K=512 SC, reference default frozen set @ %.1f dB "
+                      "(the reference's published polar throughput configuration)" % args.snr,
+               value=B * rt.world * args.steps * K / dt / 1e6, unit="info-Mbps", ms_per_step=dt / args.steps * 1e3,
+               kernel_ms=kms, frames_per_gpu=B, fer=float(c[1]) / max(1, c[2]), **rank_fields(pr, args.steps, c),
+               published_reference=dict(value=0.003983, unit="Mbps",
+                                        source="benchmarks/results/data/throughput_results.json:4-14 "
+                                               "(reference hardware, NumPy, one frame at a time)"),
+               roofline=roofline("polar_sc_1024_default", polar_kernel_name(dec.plan, 10), B, 8 * N + K, kms))
     if pool is not None:
         from oracle import oracle as O
         from oracle import refnumpy as R
-        S = args.cpu_frames_numpy
-        llr_h = llr[:max(S, args.cpu_frames)].cpu().numpy()
-        got = out[:llr_h.shape[0]].cpu().numpy().astype(np.int64)
+        S, S1, S2 = 1024, 64, 16384
+        lh = llr[:S2].cpu().numpy()
+        got = out[:S2].cpu().numpy().astype(np.int64)
+        fr = dec.frozen_bits
         procs = cpu_processes()
-        res["cpu_baseline"] = numpy_baseline(
-            pool, procs, "SCL N=1024 L=%d" % L,
-            lambda: R.polar_batch(N, L, frozen, llr_h[:S], pool=pool), S, K, got[:S])
-        S2 = args.cpu_frames
-        t0 = time.perf_counter()
-        ref = O.scl_decode(N, L, frozen, llr_h[:S2], threads=procs)
-        ct = time.perf_counter() - t0
-        res["cpu_baseline"]["c_port"] = dict(
-            value=S2 * K / ct / 1e6, unit="info-Mbps", cores=procs, kind="port",
-            sample="first %d frames, oracle/refcpu.c SCL L=%d (loop-faithful C restatement), OpenMP %d threads, "
-                   "%.1f s" % (S2, L, procs, ct),
-            mismatching_frames_vs_gpu=int((ref != got[:S2]).any(axis=1).sum()))
+        res["cpu_baseline"] = numpy_baseline(pool, procs, "SC N=1024, default frozen set",
+                                             lambda: R.polar_batch(N, 0, fr, lh[:S], pool=pool), S, K, got[:S],
+                                             single=(lambda: R.polar_batch(N, 0, fr, lh[:S1]), S1))
+        c_port(res["cpu_baseline"], "SC", lambda: O.sc_decode(N, fr, lh, threads=procs), S2, K, got, procs)
+    del llr, out, msg
+    return res
+
+
+def bench_config0(args, rt, pool):
+    """BASELINE configs[0]: polar N=256 K=128 SC, 100 frames @ 3 dB, made as
+    benchmarks/throughput_test.py:196-228 makes them (PolarEncoder default
+    frozen set, AWGNChannel(3.0, seed=42), 10 warm-up frames, then 100 random
+    messages; tests/test_host.py pins this replay to the reference's own
+    frames).  The reference decodes them one at a time in NumPy on one core;
+    here the 100 frames are one GPU batch (launch-latency bound: a plumbing
+    figure, not a throughput claim)."""
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    from polarcode_and_ldpc_amd.polar import PolarEncoder, SCDecoder
+    N, K, F = 256, 128, 100
+    state = np.random.get_state()
+    enc = PolarEncoder(N, K)
+    ch = AWGNChannel(snr_db=3.0, seed=42)
+    for _ in range(10):
+        ch.transmit(enc.encode(np.random.randint(0, 2, K)), return_llr=True)
+    msgs = np.array([np.random.randint(0, 2, K) for _ in range(F)])
+    llr_h = np.array([ch.transmit(enc.encode(m), return_llr=True) for m in msgs])
+    np.random.set_state(state)
+    dec = SCDecoder(N, K, frozen_bits=enc.get_frozen_bits_positions())
+    llr = torch.from_numpy(llr_h).cuda()
+    out = torch.empty((F, K), dtype=torch.uint8, device="cuda")
+    kt = KernelTimer()
+    dt, pr = timed_steps(lambda: kt(lambda: dec.plan.decode(llr, out)), args.steps, args.warmup, rt,
+                         on_timed=kt.reset)
+    got = out.cpu().numpy().astype(np.int64)
+    res = dict(metric="decoded info-Mbps, polar N=256 K=128 SC, the 100 throughput_test.py frames @ 3 dB "
+                      "(BASELINE configs[0])", value=F * rt.world * args.steps * K / dt / 1e6, unit="info-Mbps",
+               ms_per_step=dt / args.steps * 1e3, kernel_ms=kt.mean_ms(), frames=F,
+               rank_ms_per_step=[t / args.steps * 1e3 for t in pr],
+               frame_errors=int((got != msgs).any(axis=1).sum()),
+               roofline=roofline("polar_sc_256", polar_kernel_name(dec.plan, 8), F, 8 * N + K, kt.mean_ms()))
+    if pool is not None:
+        from oracle import refnumpy as R
+        fr = dec.frozen_bits
+        res["cpu_baseline"] = numpy_baseline(pool, cpu_processes(), "SC N=256, the 100 configs[0] frames",
+                                             lambda: R.polar_batch(N, 0, fr, llr_h, pool=pool), F, K, got,
+                                             single=(lambda: R.polar_batch(N, 0, fr, llr_h), F))
+        res["cpu_baseline"]["note"] = "single_core is the reference configuration itself (one process, NumPy)"
     return res
 
 
@@ -370,13 +546,14 @@ def bench_ldpc(args, rt, pool):
     out = torch.empty((B, n), dtype=torch.uint8, device="cuda")
     its = torch.empty((B,), dtype=torch.int32, device="cuda")
     dt, per_rank, kms, c = decode_loop(rt, plan, llr, out, cw, k, args.steps, args.warmup, its)
+    counted = rank_fields(per_rank, args.steps, c)
     kname = {2: "ldpc_reg_kernel<BP,DV=3>", 1: "ldpc_decode_kernel<BP>", 3: "ldpc_check_kernel<BP>"}.get(
         plan.info.reserved, "?")
     res = dict(metric="decoded info-Mbps, LDPC (504,252) BP max_iter=20, reference-harness frames @ %.1f dB"
                       % args.snr,
                value=B * rt.world * args.steps * k / dt / 1e6, unit="info-Mbps", ms_per_step=dt / args.steps * 1e3,
                rank_ms_per_step=[t / args.steps * 1e3 for t in per_rank], kernel_ms=kms,
-               mean_iterations=float(its.double().mean().item()),
+               frames_counted=counted["frames_counted"], mean_iterations=float(its.double().mean().item()),
                roofline=roofline("ldpc_bp_504", kname, B, 9 * n, kms))
     res["roofline"]["limit"] = "VALU issue (fp64 transcendentals): see roofline.valu"
     if "ldpc_valid" in args.sec:
@@ -384,38 +561,42 @@ def bench_ldpc(args, rt, pool):
         # codeword-symmetric) at the same SNR, early stop on.
         llr0 = AWGNChannel(args.snr).llr_batch_device(None, n, B, seed=4243, frame_offset=rt.rank * B)
         out0, its0 = torch.empty_like(out), torch.empty_like(its)
-        dt0, _ = timed_steps(lambda: plan.decode(llr0, out0, its0), args.steps, args.warmup, rt)
+        dt0, pr0 = timed_steps(lambda: plan.decode(llr0, out0, its0), args.steps, args.warmup, rt)
         res["valid_codewords"] = dict(value=B * rt.world * args.steps * k / dt0 / 1e6, unit="info-Mbps",
                                       ms_per_step=dt0 / args.steps * 1e3,
+                                      rank_ms_per_step=[t / args.steps * 1e3 for t in pr0],
                                       mean_iterations=float(its0.double().mean().item()),
                                       bit_errors=int(out0.sum().item()),
                                       what="all-zero codeword frames (device AWGN), BP max_iter=20, early stop")
+        if pool is not None:
+            from oracle import refnumpy as R
+            S = args.cpu_frames_numpy
+            lh = llr0[:S].cpu().numpy()
+            res["valid_codewords"]["cpu_baseline"] = numpy_baseline(
+                pool, cpu_processes(), "BP-20 (504,252), all-zero codewords, early stop",
+                lambda: R.ldpc_batch(enc.H, lh, "bp", 20, True, pool=pool)[0], S, k,
+                out0[:S].cpu().numpy().astype(np.int64))
         del llr0, out0, its0
     if pool is not None:
         from oracle import oracle as O
         from oracle import refnumpy as R
         from polarcode_and_ldpc_amd.ldpc import dense_to_csr
-        S = args.cpu_frames_numpy
-        llr_h = llr[:max(S, args.cpu_frames_ldpc)].cpu().numpy()
+        S, S1, S2 = args.cpu_frames_numpy, 8, args.cpu_frames_ldpc
+        llr_h = llr[:max(S, S2)].cpu().numpy()
         got = out[:llr_h.shape[0]].cpu().numpy().astype(np.int64)
         procs = cpu_processes()
         res["cpu_baseline"] = numpy_baseline(
             pool, procs, "BP-20 (504,252)", lambda: R.ldpc_batch(enc.H, llr_h[:S], "bp", 20, True, pool=pool)[0],
-            S, k, got[:S])
-        S2 = args.cpu_frames_ldpc
+            S, k, got[:S], single=(lambda: R.ldpc_batch(enc.H, llr_h[:S1], "bp", 20, True)[0], S1))
         rp, ci = dense_to_csr(enc.H)
-        t0 = time.perf_counter()
-        rb, _ = O.ldpc_decode(rp, ci, n, llr_h[:S2], "bp", 20, True, 1.0, threads=procs)
-        ct = time.perf_counter() - t0
-        res["cpu_baseline"]["c_port"] = dict(
-            value=S2 * k / ct / 1e6, unit="info-Mbps", cores=procs, kind="port",
-            sample="first %d frames, oracle/refcpu.c BP-20, OpenMP %d threads, %.1f s" % (S2, procs, ct),
-            mismatching_frames_vs_gpu=int((rb != got[:S2]).any(axis=1).sum()))
+        c_port(res["cpu_baseline"], "BP-20",
+               lambda: O.ldpc_decode(rp, ci, n, llr_h[:S2], "bp", 20, True, 1.0, threads=procs)[0], S2, k,
+               got[:S2], procs)
     return res
 
 
 # ---------------------------------------------------------------- configs[3], configs[4]
-def bench_cascl(args, rt):
+def bench_cascl(args, rt, pool=None):
     """BASELINE configs[3]: CA-SCL N=1024 K=512 L=32 + CRC-8 (the CRC is inside
     the K info bits, src/polar/encoder.py:74-78)."""
     from polarcode_and_ldpc_amd import _native
@@ -436,12 +617,30 @@ def bench_cascl(args, rt):
     del cw
     out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
     steps = min(args.steps, args.extra_steps)
-    dt, _, kms, c = decode_loop(rt, dec.plan, llr, out, msg, K, steps, 1)
+    dt, pr, kms, c = decode_loop(rt, dec.plan, llr, out, msg, K, steps, 1)
     res = dict(metric="decoded info-Mbps, CA-SCL N=1024 K=512 L=32 + CRC-8 (BASELINE configs[3]) @ 1.0 dB",
                value=B * rt.world * steps * K / dt / 1e6, unit="info-Mbps", steps=steps,
-               ms_per_step=dt / steps * 1e3, kernel_ms=kms, frames_per_gpu=B,
+               ms_per_step=dt / steps * 1e3, kernel_ms=kms, frames_per_gpu=B, **rank_fields(pr, steps, c),
                ber=float(c[0]) / max(1, c[2] * K), fer=float(c[1]) / max(1, c[2]),
                roofline=roofline("polar_cascl_1024_l32", polar_kernel_name(dec.plan, 10), B, 8 * N + K, kms))
+    if pool is not None:
+        # the C restatement of CA-SCL (oracle/refcpu.c) on 64 frames of the same
+        # batch, against the GPU's CA-SCL bits; the reference's own NumPy path
+        # for these frames is its plain SCLDecoder (use_crc is inert, decoder.py:
+        # 202-203, 259), timed on 32 frames against a GPU plain-SCL decode of them
+        from oracle import oracle as O
+        from oracle import refnumpy as R
+        from polarcode_and_ldpc_amd.polar import SCLDecoder
+        S, S2 = args.cpu_frames_l32, 64
+        lh = llr[:max(S, S2)].cpu().numpy()
+        procs = cpu_processes()
+        plain = SCLDecoder(N, K, L, frozen_bits=fr).decode_batch(torch.from_numpy(lh[:S]).cuda())
+        res["cpu_baseline"] = numpy_baseline(pool, procs, "plain SCL N=1024 L=32 (the reference's SCLDecoder; "
+                                             "use_crc inert)", lambda: R.polar_batch(N, L, fr, lh[:S], pool=pool), S,
+                                             K, plain.cpu().numpy().astype(np.int64))
+        c_port(res["cpu_baseline"], "CA-SCL L=32 CRC-8",
+               lambda: O.cascl_decode(N, L, fr, lh[:S2], "CRC-8", threads=procs), S2, K,
+               out[:S2].cpu().numpy().astype(np.int64), procs)
     del llr, out, msg
     if "sweep" in args.sec:
         t0 = time.perf_counter()
@@ -458,35 +657,46 @@ def bench_cascl(args, rt):
     return res
 
 
-def bench_long(args, rt):
+def bench_long(args, rt, pool=None):
     """BASELINE configs[4] per GPU: 1 M frames over 8 GPUs = 131 072 frames each."""
     B = args.long_batch
     steps = min(args.steps, args.extra_steps)
     res = {}
     if "long_polar" in args.sec:
-        res.update(_long_polar(rt, B, steps))
+        res.update(_long_polar(rt, B, steps, pool))
     for es in (True, False):
         if ("long_ms" if es else "long_ms_noes") in args.sec:
-            res.update(_long_ms(rt, B, steps, es))
+            res.update(_long_ms(rt, B, steps, es, pool))
     return res
 
 
-def _long_polar(rt, B, steps):
+def _long_polar(rt, B, steps, pool=None):
     N, K = 4096, 2048
     dec, _, msg, llr = polar_fixture(rt, N, K, 8, B, 1.0, 45)
     out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
-    dt, _, kms, c = decode_loop(rt, dec.plan, llr, out, msg, K, steps, 1)
+    dt, pr, kms, c = decode_loop(rt, dec.plan, llr, out, msg, K, steps, 1)
     res = {"polar_4096_l8": dict(
         metric="decoded info-Mbps, polar N=4096 K=2048 SCL L=8 @ 1.0 dB", value=B * rt.world * steps * K / dt / 1e6,
         unit="info-Mbps", steps=steps, ms_per_step=dt / steps * 1e3, kernel_ms=kms, frames_per_gpu=B,
-        llr_bytes_per_gpu=B * N * 8, fer=float(c[1]) / max(1, c[2]),
+        llr_bytes_per_gpu=B * N * 8, fer=float(c[1]) / max(1, c[2]), **rank_fields(pr, steps, c),
         roofline=roofline("polar_scl_4096_l8", polar_kernel_name(dec.plan, 12), B, 8 * N + K, kms))}
+    if pool is not None:
+        from oracle import oracle as O
+        from oracle import refnumpy as R
+        S, S2 = 16, 128
+        lh = llr[:S2].cpu().numpy()
+        got = out[:S2].cpu().numpy().astype(np.int64)
+        procs = cpu_processes()
+        fr = dec.frozen_bits
+        r = res["polar_4096_l8"]["cpu_baseline"] = numpy_baseline(
+            pool, procs, "SCL N=4096 L=8", lambda: R.polar_batch(N, 8, fr, lh[:S], pool=pool), S, K, got[:S])
+        c_port(r, "SCL N=4096 L=8", lambda: O.scl_decode(N, 8, fr, lh, threads=procs), S2, K, got, procs)
     del dec, msg, llr, out
     torch.cuda.empty_cache()
     return res
 
 
-def _long_ms(rt, B, steps, es):
+def _long_ms(rt, B, steps, es, pool=None):
     from polarcode_and_ldpc_amd.channel import AWGNChannel
     from polarcode_and_ldpc_amd.ldpc import MSDecoder
     from polarcode_and_ldpc_amd.ldpc.matrix import regular_construction
@@ -498,14 +708,29 @@ def _long_ms(rt, B, steps, es):
     out = torch.empty((B, n), dtype=torch.uint8, device="cuda")
     its = torch.empty((B,), dtype=torch.int32, device="cuda")
     zero = torch.zeros((B, k), dtype=torch.uint8, device="cuda")
-    dt, _, kms, c = decode_loop(rt, dec.plan, llr, out, zero, k, steps, 1, its)
+    dt, pr, kms, c = decode_loop(rt, dec.plan, llr, out, zero, k, steps, 1, its)
     res = {"ldpc_8192_ms20" + ("" if es else "_no_early_stop"): dict(
         metric="decoded info-Mbps, LDPC n=8192 (3,6)-regular min-sum max_iter=20, all-zero codeword @ 1.5 dB, "
                "early stop %s" % ("on" if es else "off"),
         value=B * rt.world * steps * k / dt / 1e6, unit="info-Mbps", steps=steps, ms_per_step=dt / steps * 1e3,
         kernel_ms=kms, frames_per_gpu=B, mean_iterations=float(its.double().mean().item()),
-        llr_bytes_per_gpu=B * n * 8, fer=float(c[1]) / max(1, c[2]),
+        llr_bytes_per_gpu=B * n * 8, fer=float(c[1]) / max(1, c[2]), **rank_fields(pr, steps, c),
         roofline=roofline("ldpc_ms_8192" + ("" if es else "_noes"), "ldpc_ms_compact_kernel", B, 9 * n, kms))}
+    if pool is not None:
+        from oracle import oracle as O
+        from oracle import refnumpy as R
+        from polarcode_and_ldpc_amd.ldpc import dense_to_csr
+        S, S2 = 16, 512
+        lh = llr[:S2].cpu().numpy()
+        got = out[:S2].cpu().numpy().astype(np.int64)
+        procs = cpu_processes()
+        key = next(iter(res))
+        r = res[key]["cpu_baseline"] = numpy_baseline(
+            pool, procs, "MS-20 n=8192 early stop %s" % ("on" if es else "off"),
+            lambda: R.ldpc_batch(H, lh[:S], "ms", 20, es, 1.0, pool=pool)[0], S, k, got[:S])
+        rp, ci = dense_to_csr(H)
+        c_port(r, "MS-20 n=8192", lambda: O.ldpc_decode(rp, ci, n, lh, "ms", 20, es, 1.0, threads=procs)[0], S2, k,
+               got, procs)
     del llr, out, its, zero, dec
     torch.cuda.empty_cache()
     return res
@@ -570,6 +795,7 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=4096, help="frames for the C-port baseline (polar)")
     ap.add_argument("--cpu-frames-ldpc", type=int, default=32768, help="frames for the C-port baseline (LDPC)")
     ap.add_argument("--cpu-frames-numpy", type=int, default=256, help="frames for the NumPy baseline")
+    ap.add_argument("--cpu-frames-l32", type=int, default=32, help="frames for the NumPy SCL L=32 baseline")
     ap.add_argument("--long-batch", type=int, default=131072, help="configs[4] frames per GPU (1 M / 8)")
     ap.add_argument("--extra-steps", type=int, default=5, help="cap on timed steps of the configs[3]/[4] keys")
     ap.add_argument("--sweep-frames", type=int, default=131072)
@@ -619,28 +845,32 @@ def main():
         from oracle import refnumpy as R
         pool = R.make_pool(cpu_processes())
     pol = bench_polar(args, rt, pool)
+    extra = {}
+    if "sc_default" in args.sec:
+        extra["polar_sc_default"] = bench_sc_default(args, rt, pool)
+    if "config0" in args.sec:
+        extra["config0_sc_256"] = bench_config0(args, rt, pool)
     ldp = bench_ldpc(args, rt, pool) if "ldpc" in args.sec else None
+    if "cascl" in args.sec:
+        extra["cascl_l32"] = bench_cascl(args, rt, pool)
+    if args.sec & {"long_polar", "long_ms", "long_ms_noes"}:
+        extra["long_block"] = bench_long(args, rt, pool)
     if pool is not None:
         pool.close()
-    extra = {}
-    if "cascl" in args.sec:
-        extra["cascl_l32"] = bench_cascl(args, rt)
-    if args.sec & {"long_polar", "long_ms", "long_ms_noes"}:
-        extra["long_block"] = bench_long(args, rt)
     if rt.rank == 0:
         line = {
-            "metric": METRIC, "value": pol["value"], "unit": "info-Mbps", "n_gpus": rt.world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": pol["ms_per_step"],
-            "rank_ms_per_step": pol["rank_ms_per_step"],
+            "metric": METRIC, "value": pol.get("value"), "unit": "info-Mbps", "n_gpus": rt.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": pol.get("ms_per_step"),
+            "rank_ms_per_step": pol.get("rank_ms_per_step"),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: random messages, device polar encoder, device AWGN (Philox) at %.1f dB Es/N0" % args.snr,
             "config": {"workload": "polar N=1024 K=512 SCL L=%d decode (BASELINE configs[1]), bit-reversed "
                                    "Bhattacharyya(2 dB) frozen set" % args.list_size,
                        "global_batch": args.batch * rt.world, "frames_per_gpu": args.batch,
                        "parallelism": "frame-sharded x%d (one RCCL all-reduce of error counters per step)" % rt.world},
-            "roofline": pol["roofline"],
+            "roofline": pol.get("roofline"),
             "cpu_baseline": pol.get("cpu_baseline"),
-            "ber": pol["ber"], "fer": pol["fer"], "plan": pol["plan"],
+            "ber": pol.get("ber"), "fer": pol.get("fer"), "plan": pol.get("plan"),
             "end_to_end": pol.get("end_to_end"),
             "default_frozen_set": pol.get("default_frozen_set"),
         }

@@ -115,14 +115,28 @@ int pl_decode_ws(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld
                  int32_t* iters_dev, void* workspace_dev, int64_t workspace_bytes, void* stream);
 
 /* Pre-allocate `stream`'s workspace for batches up to max_batch, so that
- * pl_decode on that stream never allocates. */
+ * pl_decode on that stream never allocates (max_batch == 0: pl_plan_release).
+ * If the device cannot hold the full-speed size, the largest halving of at
+ * least one unit is kept (fewer resident wavefronts, same results). */
 int pl_plan_reserve(pl_plan* plan, int64_t max_batch, void* stream);
+
+/* Free `stream`'s workspace (after draining that stream).  A finished stream's
+ * buffer is otherwise kept until pl_plan_destroy, invisible to torch's
+ * caching allocator.  No-op for a stream the plan has not decoded on. */
+int pl_plan_release(pl_plan* plan, void* stream);
+
+/* Number of per-stream workspaces the plan holds and their total bytes. */
+int pl_plan_workspace_stats(const pl_plan* plan, int64_t* streams, int64_t* bytes);
 
 int pl_plan_get_info(const pl_plan* plan, pl_plan_info* info);
 int pl_plan_destroy(pl_plan* plan);
 const char* pl_last_error(void);
 
-/* Diagnostic: pl_decode of a polar plan through an instrumented kernel that adds
+/* Every call taking a plan must run with the plan's device current (the device
+ * current at plan creation); otherwise it returns PL_EINVAL and does nothing. */
+
+/* Diagnostic build only (make DIAG=1; the product library returns
+ * PL_EUNSUPPORTED): pl_decode of a polar plan through an instrumented kernel that adds
  * per-phase s_memtime cycle totals (summed over all frames) into stamps_dev[8]:
  * tree kernel (pl_plan_info.reserved == 4): [0] fused top, [1] workspace chains,
  * [2] LDS chain, [3] path metrics, [4] pruning/cloning, [5] partial-sum walk,
@@ -130,6 +144,10 @@ const char* pl_last_error(void);
  * pl_decode; read shares. */
 int pl_debug_polar_stamps(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
                           unsigned long long* stamps_dev, void* stream);
+
+/* Test hook: overwrite the device id a plan is bound to, so the wrong-device
+ * check can be exercised on a one-GPU machine.  Not for production use. */
+int pl_debug_set_plan_device(pl_plan* plan, int32_t device);
 
 /* ---- Monte-Carlo frame source (replaces src/channel/awgn.py:91-112 and the
  *      message/encode loop of benchmarks/ber_simulation.py:167-177) ---------- */
@@ -146,7 +164,7 @@ int pl_polar_encode(const pl_plan* plan, const uint8_t* msg_dev, int64_t batch, 
                     void* stream);
 
 /* BPSK (0 -> +1, 1 -> -1) + AWGN with sigma = sqrt(1/(2*10^(snr_db/10)))
- * (awgn.py:27-32, :47, :88), LLR = 2*y/sigma^2 (:75).  codeword_dev uint8
+ * (awgn.py:27-32, :47, :88), LLR = 2*y/sigma^2 (:75).  codeword_dev uint8 (bit 0 of each byte)
  * [batch][n] or NULL for the all-zero codeword.  Noise: Philox4x32-10 keyed by
  * (seed, frame_offset + b) + Box-Muller; statistically equivalent to the
  * reference's np.random.normal, not stream-identical. */

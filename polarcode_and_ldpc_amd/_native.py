@@ -24,6 +24,7 @@ EXPORTS = (
     "pl_plan_destroy", "pl_last_error", "pl_random_bits", "pl_polar_encode", "pl_awgn_llr",
     "pl_count_errors", "pl_debug_polar_stamps", "pl_polar_plan_set_crc", "pl_crc_append",
     "pl_rayleigh_llr", "pl_bsc", "pl_gf2_encode", "pl_decode_ws", "pl_plan_workspace_bytes",
+    "pl_plan_release", "pl_plan_workspace_stats", "pl_debug_set_plan_device",
 )
 
 
@@ -48,6 +49,9 @@ def _load():
     L.pl_plan_reserve.argtypes = [P, I64, P]
     L.pl_decode_ws.argtypes = [P, P, I64, I64, P, P, P, I64, P]
     L.pl_plan_workspace_bytes.argtypes = [P, I64, ctypes.POINTER(ctypes.c_int64)]
+    L.pl_plan_release.argtypes = [P, P]
+    L.pl_plan_workspace_stats.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    L.pl_debug_set_plan_device.argtypes = [P, I32]
     L.pl_plan_get_info.argtypes = [P, ctypes.POINTER(PlanInfo)]
     L.pl_plan_destroy.argtypes = [P]
     L.pl_last_error.restype = ctypes.c_char_p
@@ -67,6 +71,18 @@ def _load():
 
 
 lib = _load()
+_BUILD_ID = None
+
+
+def build_id() -> str:
+    """Digest of the loaded libpolarldpc.so (keys resumable result logs to the
+    decoder build that produced them)."""
+    global _BUILD_ID
+    if _BUILD_ID is None:
+        import hashlib
+        with open(LIB_PATH, "rb") as f:
+            _BUILD_ID = hashlib.sha1(f.read()).hexdigest()[:16]
+    return _BUILD_ID
 
 
 class NativeError(RuntimeError):
@@ -123,6 +139,16 @@ class Plan:
     def reserve(self, max_batch: int, stream=None):
         """Pre-size `stream`'s workspace (default: torch's current stream)."""
         check(lib.pl_plan_reserve(self._h, int(max_batch), ctypes.c_void_p(_stream(stream))), "pl_plan_reserve")
+
+    def release(self, stream=None):
+        """Free `stream`'s workspace (default: torch's current stream)."""
+        check(lib.pl_plan_release(self._h, ctypes.c_void_p(_stream(stream))), "pl_plan_release")
+
+    def workspace_stats(self):
+        """(streams with a workspace, their total bytes)."""
+        n, b = ctypes.c_int64(), ctypes.c_int64()
+        check(lib.pl_plan_workspace_stats(self._h, ctypes.byref(n), ctypes.byref(b)), "pl_plan_workspace_stats")
+        return int(n.value), int(b.value)
 
     def workspace_bytes(self, batch: int) -> int:
         b = ctypes.c_int64()

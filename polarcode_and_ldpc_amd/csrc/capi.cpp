@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -17,9 +18,15 @@
 
 // Device workspace of one stream (polar: per resident wavefront; LDPC codes
 // whose messages exceed LDS: per frame of a chunk).  Grown lazily to the batch.
+// Its own mutex serialises the decodes of that stream only, so a stream that
+// drains and regrows its buffer never stalls decodes on other streams.
 struct Workspace {
+    std::mutex mu;
     void* ptr = nullptr;
     size_t bytes = 0;
+    ~Workspace() {
+        if (ptr) hipFree(ptr);  // hipFree waits for work that still uses it
+    }
 };
 
 struct pl_plan {
@@ -48,8 +55,8 @@ struct pl_plan {
     // frame), one buffer per stream (plans are shared across host threads that
     // use distinct streams; a decode only ever touches its stream's buffer)
     size_t ws_unit = 0;
-    std::mutex mu;
-    std::unordered_map<hipStream_t, Workspace> ws;
+    std::mutex mu;  // guards the map only; each entry has its own mutex
+    std::unordered_map<hipStream_t, std::shared_ptr<Workspace>> ws;
 };
 
 static thread_local std::string g_err;
@@ -87,6 +94,19 @@ static hipError_t upload(T** dst, const std::vector<T>& src) {
 static int env_int(const char* name, int dflt) {
     const char* s = std::getenv(name);
     return (s && *s) ? std::atoi(s) : dflt;
+}
+
+// Every call that touches a plan's device memory must run on the plan's device
+// (the one current at plan creation): a workspace allocated, or a kernel
+// launched, on another device would use foreign pointers.
+static int check_device(const pl_plan* p) {
+    int cur = -1;
+    const hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess) return hipfail(e, "hipGetDevice");
+    if (cur != p->device)
+        return fail(PL_EINVAL, "current device " + std::to_string(cur) + " is not the plan's device " +
+                                   std::to_string(p->device) + " (hipSetDevice first)");
+    return PL_OK;
 }
 
 static int device_cus(int dev) {
@@ -236,9 +256,9 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     const size_t lds_all = (size_t)2 * (size_t)E * 8 + lds_small;  // + T[E], C[E]
     g.use_global = lds_all > 64 * 1024 ? 1 : 0;
     g.lds_bytes = (int)(((g.use_global ? lds_small : lds_all) + 15) & ~(size_t)15);
-    // check-per-thread kernel (ldpc.hip ldpc_check_kernel): diagnostic, PL_LDPC_KERNEL=check
+    // check-per-thread kernel (ldpc.hip ldpc_check_kernel): diagnostic build only, PL_LDPC_KERNEL=check
     const char* lk = std::getenv("PL_LDPC_KERNEL");
-    g.check_kernel = !g.use_global && lk && std::string(lk) == "check" ? 1 : 0;
+    g.check_kernel = PL_DIAG && !g.use_global && lk && std::string(lk) == "check" ? 1 : 0;
     // register-cached kernel: constant variable degree < 8, LDS-resident state
     g.reg_variant = 0;
     if (!g.use_global && !g.check_kernel && !(lk && std::string(lk) == "generic")) {
@@ -354,28 +374,41 @@ static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld,
     return PL_OK;
 }
 
-// The calling stream's workspace, grown to `need` bytes.  A buffer is only
-// ever used by its own stream, so before it is replaced only that stream has
-// to drain.  Caller holds p->mu.
-static int stream_ws(pl_plan* p, hipStream_t s, size_t need, Workspace** out) {
-    Workspace& w = p->ws[s];
-    if (w.bytes < need) {
-        if (w.ptr) {
-            hipError_t e = hipStreamSynchronize(s);
-            if (e != hipSuccess) return hipfail(e, "workspace regrow: stream synchronize");
-            hipFree(w.ptr);
-            w.ptr = nullptr;
-            w.bytes = 0;
-        }
-        hipError_t e = hipMalloc(&w.ptr, need);
-        if (e != hipSuccess) {
-            w.ptr = nullptr;
-            return hipfail(e, "decode workspace");
-        }
-        w.bytes = need;
+// The calling stream's workspace entry (created empty on first use).
+static std::shared_ptr<Workspace> stream_entry(pl_plan* p, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    std::shared_ptr<Workspace>& w = p->ws[s];
+    if (!w) w = std::make_shared<Workspace>();
+    return w;
+}
+
+// Grow `w` (its mutex held by the caller) to `need` bytes.  A buffer is only
+// ever used by its own stream, so before it is replaced only that stream has to
+// drain.  If the device cannot hold `need`, fall back to the largest halving
+// that is still at least one unit (the decode then runs fewer resident
+// wavefronts / smaller chunks, decode_impl clamps to what the buffer holds).
+static int grow_ws(pl_plan* p, Workspace* w, hipStream_t s, size_t need) {
+    if (w->bytes >= need) return PL_OK;
+    if (w->ptr) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hipfail(e, "workspace regrow: stream synchronize");
+        hipFree(w->ptr);
+        w->ptr = nullptr;
+        w->bytes = 0;
     }
-    *out = &w;
-    return PL_OK;
+    const size_t unit = std::max<size_t>(p->ws_unit, 1);
+    size_t want = need;
+    for (;;) {
+        hipError_t e = hipMalloc(&w->ptr, want);
+        if (e == hipSuccess) {
+            w->bytes = want;
+            return PL_OK;
+        }
+        w->ptr = nullptr;
+        (void)hipGetLastError();  // clear the sticky allocation error before retrying
+        if (e != hipErrorOutOfMemory || want <= unit) return hipfail(e, "decode workspace");
+        want = std::max(unit, (want / 2) / unit * unit);
+    }
 }
 
 static int check_decode_args(const pl_plan* p, int64_t batch, int64_t ld, const void* llr, const void* bits) {
@@ -389,11 +422,50 @@ static int check_decode_args(const pl_plan* p, int64_t batch, int64_t ld, const 
 
 extern "C" int pl_plan_reserve(pl_plan* p, int64_t max_batch, void* stream) {
     if (!p) return fail(PL_EINVAL, "plan is NULL");
+    if (max_batch < 0) return fail(PL_EINVAL, "max_batch < 0");
+    if (max_batch == 0) return pl_plan_release(p, stream);
+    int rc = check_device(p);
+    if (rc) return rc;
     const size_t need = ws_need(p, max_batch);
     if (need == 0) return PL_OK;
-    std::lock_guard<std::mutex> lk(p->mu);
-    Workspace* w;
-    return stream_ws(p, (hipStream_t)stream, need, &w);
+    const hipStream_t s = (hipStream_t)stream;
+    std::shared_ptr<Workspace> w = stream_entry(p, s);
+    std::lock_guard<std::mutex> lk(w->mu);
+    return grow_ws(p, w.get(), s, need);
+}
+
+extern "C" int pl_plan_release(pl_plan* p, void* stream) {
+    if (!p) return fail(PL_EINVAL, "plan is NULL");
+    const hipStream_t s = (hipStream_t)stream;
+    std::shared_ptr<Workspace> w;
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        auto it = p->ws.find(s);
+        if (it == p->ws.end()) return PL_OK;
+        w = it->second;
+        p->ws.erase(it);
+    }
+    std::lock_guard<std::mutex> lk(w->mu);  // a decode in flight on this stream finishes its launch first
+    if (w->ptr) {
+        hipError_t e = hipStreamSynchronize(s);
+        hipFree(w->ptr);
+        w->ptr = nullptr;
+        w->bytes = 0;
+        if (e != hipSuccess) return hipfail(e, "workspace release: stream synchronize");
+    }
+    return PL_OK;
+}
+
+extern "C" int pl_plan_workspace_stats(const pl_plan* p, int64_t* streams, int64_t* bytes) {
+    if (!p || !streams || !bytes) return fail(PL_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(const_cast<pl_plan*>(p)->mu);
+    *streams = 0;
+    *bytes = 0;
+    for (const auto& kv : p->ws) {
+        ++*streams;
+        *bytes += (int64_t)kv.second->bytes;  // racy read of a size_t, diagnostic only
+    }
+    return PL_OK;
 }
 
 extern "C" int pl_plan_workspace_bytes(const pl_plan* p, int64_t batch, int64_t* bytes) {
@@ -407,12 +479,14 @@ extern "C" int pl_decode(pl_plan* p, const double* llr, int64_t batch, int64_t l
                          int32_t* iters, void* stream) {
     int rc = check_decode_args(p, batch, ld, llr, bits);
     if (rc || batch == 0) return rc;
-    hipStream_t s = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(p->mu);
+    if ((rc = check_device(p))) return rc;
+    const hipStream_t s = (hipStream_t)stream;
     const size_t need = ws_need(p, batch);
-    Workspace* w = nullptr;
-    if (need && (rc = stream_ws(p, s, need, &w))) return rc;
-    return decode_impl(p, llr, batch, ld, bits, iters, w ? w->ptr : nullptr, w ? w->bytes : 0, nullptr, s);
+    if (!need) return decode_impl(p, llr, batch, ld, bits, iters, nullptr, 0, nullptr, s);
+    std::shared_ptr<Workspace> w = stream_entry(p, s);
+    std::lock_guard<std::mutex> lk(w->mu);
+    if ((rc = grow_ws(p, w.get(), s, need))) return rc;
+    return decode_impl(p, llr, batch, ld, bits, iters, w->ptr, w->bytes, nullptr, s);
 }
 
 extern "C" int pl_decode_ws(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
@@ -420,6 +494,7 @@ extern "C" int pl_decode_ws(pl_plan* p, const double* llr, int64_t batch, int64_
     int rc = check_decode_args(p, batch, ld, llr, bits);
     if (rc || batch == 0) return rc;
     if (workspace_bytes < 0) return fail(PL_EINVAL, "workspace_bytes < 0");
+    if ((rc = check_device(p))) return rc;
     return decode_impl(p, llr, batch, ld, bits, iters, workspace, (size_t)workspace_bytes, nullptr,
                        (hipStream_t)stream);
 }
@@ -427,19 +502,32 @@ extern "C" int pl_decode_ws(pl_plan* p, const double* llr, int64_t batch, int64_
 extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
                                      unsigned long long* stamps_dev, void* stream) {
     if (!p || p->kind != 0 || !stamps_dev) return fail(PL_EINVAL, "polar plan and stamp buffer required");
+#if !PL_DIAG
+    (void)llr; (void)batch; (void)ld; (void)bits; (void)stream;
+    return fail(PL_EUNSUPPORTED, "stamped kernels are in the diagnostic build only (make DIAG=1)");
+#else
     int rc = check_decode_args(p, batch, ld, llr, bits);
     if (rc || batch == 0) return rc;
-    hipStream_t s = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(p->mu);
-    Workspace* w = nullptr;
-    if ((rc = stream_ws(p, s, ws_need(p, batch), &w))) return rc;
+    if ((rc = check_device(p))) return rc;
+    const hipStream_t s = (hipStream_t)stream;
+    std::shared_ptr<Workspace> w = stream_entry(p, s);
+    std::lock_guard<std::mutex> lk(w->mu);
+    if ((rc = grow_ws(p, w.get(), s, ws_need(p, batch)))) return rc;
     return decode_impl(p, llr, batch, ld, bits, nullptr, w->ptr, w->bytes, stamps_dev, s);
+#endif
+}
+
+extern "C" int pl_debug_set_plan_device(pl_plan* p, int32_t device) {
+    if (!p) return fail(PL_EINVAL, "plan is NULL");
+    p->device = device;
+    return PL_OK;
 }
 
 extern "C" int pl_polar_plan_set_crc(pl_plan* p, int32_t crc_len, uint32_t poly) {
     if (!p || p->kind != 0) return fail(PL_EINVAL, "not a polar plan");
     if (p->sc) return fail(PL_EINVAL, "CRC-aided selection needs a list decoder (list_size >= 1)");
     if (crc_len < 0 || crc_len > 32) return fail(PL_EINVAL, "crc_len must be in [0, 32]");
+    if (int rc = check_device(p)) return rc;
     if (p->d_crc_g) { hipFree(p->d_crc_g); p->d_crc_g = nullptr; }
     if (crc_len == 0) return PL_OK;
     const int N = p->pg.N;
@@ -486,8 +574,7 @@ extern "C" int pl_plan_destroy(pl_plan* p) {
     if (p->d_pos2info) hipFree(p->d_pos2info);
     if (p->d_crc_g) hipFree(p->d_crc_g);
     if (p->d_ldpc) hipFree(p->d_ldpc);
-    for (auto& kv : p->ws)
-        if (kv.second.ptr) hipFree(kv.second.ptr);  // hipFree waits for work that still uses it
+    p->ws.clear();  // each Workspace frees its buffer (hipFree waits for work that still uses it)
     delete p;
     return PL_OK;
 }
@@ -502,6 +589,7 @@ extern "C" int pl_random_bits(uint64_t seed, int64_t frame_offset, int64_t batch
 extern "C" int pl_polar_encode(const pl_plan* p, const uint8_t* msg, int64_t batch, uint8_t* cw, void* stream) {
     if (!p || p->kind != 0) return fail(PL_EINVAL, "not a polar plan");
     if (batch < 0 || (batch > 0 && (!msg || !cw))) return fail(PL_EINVAL, "bad argument");
+    if (int rc = check_device(p)) return rc;
     const int64_t step = kMaxLaunchItems / 64;  // one wavefront per frame
     for (int64_t b0 = 0; b0 < batch; b0 += step) {
         const int64_t nb = std::min<int64_t>(step, batch - b0);

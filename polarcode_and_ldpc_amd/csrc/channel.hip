@@ -147,7 +147,8 @@ __global__ void awgn_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch
     for (int h = 0; h < 2; ++h) {
         const int j = 2 * q + h;
         if (j < n) {
-            const double s = cw ? 1.0 - 2.0 * (double)cw[b * n + j] : 1.0;  // awgn.py:47
+            // awgn.py:47 on bit 0 of the codeword byte, as the vector path reads it
+            const double s = cw ? 1.0 - 2.0 * (double)(cw[b * n + j] & 1u) : 1.0;
             const double y = s + sigma * z[h];                              // awgn.py:88
             o[j] = 2.0 * y / sigma2;                                        // awgn.py:75
         }
@@ -181,7 +182,7 @@ __global__ void rayleigh_kernel(const uint8_t* __restrict__ cw, int n, int64_t b
     normal_pair(seed, 0xFADE0001u, (uint32_t)j, f, hr, hi);
     normal_pair(seed, 0xFADE0002u, (uint32_t)j, f, z, unused);
     const double h = sqrt(0.5 * (hr * hr + hi * hi));  // |h| with unit-variance components scaled by 1/sqrt(2)
-    const double s = cw ? 1.0 - 2.0 * (double)cw[b * n + j] : 1.0;
+    const double s = cw ? 1.0 - 2.0 * (double)(cw[b * n + j] & 1u) : 1.0;  // bit 0 of the byte, as awgn_kernel
     const double y = h * s + sigma * z;
     llr[b * ld + j] = 2.0 * y * h / sigma2;
 }

@@ -5,6 +5,13 @@
 
 #define PL_DEV __device__ __forceinline__
 
+// PL_DIAG=1 (make DIAG=1, a separate library for tools/): adds the stamped /
+// alternative-geometry polar tree instances, the thread-per-check LDPC kernel
+// and the ocml BP path.  The product library (PL_DIAG=0) carries none of them.
+#ifndef PL_DIAG
+#define PL_DIAG 0
+#endif
+
 // np.sign semantics: +1 / -1 / 0 (NaN propagates).
 PL_DEV double np_sign(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : (x == 0.0 ? 0.0 : x)); }
 

@@ -569,6 +569,7 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
     if (iters && tid == 0) iters[frame] = done;
 }
 
+#if PL_DIAG
 // Thread-per-check kernel: one workgroup (256 threads) per frame, all state in
 // LDS: C[E] (check-to-variable), T[E] (check inputs), tot[n].  Checks are
 // degree-sorted by the host so a wavefront's check loops have equal length.
@@ -660,15 +661,19 @@ ldpc_check_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_
     }
 }
 
+#endif  // PL_DIAG
+
 size_t ldpc_work_bytes_per_frame(const LdpcGeom& g) {
     return g.use_global ? (size_t)(2 * (size_t)g.E) * sizeof(double) : 0;
 }
 
 template <int ALGO>
 static void* pick(bool global) {
-    const char* m = std::getenv("PL_LDPC_MATH");
+#if PL_DIAG
+    const char* m = std::getenv("PL_LDPC_MATH");  // diagnostic: ocml tanh / atanh
     if (ALGO == 0 && m && std::string(m) == "ocml")
         return global ? (void*)ldpc_decode_kernel<ALGO, true, true> : (void*)ldpc_decode_kernel<ALGO, false, true>;
+#endif
     return global ? (void*)ldpc_decode_kernel<ALGO, true, false> : (void*)ldpc_decode_kernel<ALGO, false, false>;
 }
 
@@ -681,7 +686,9 @@ static void* pick_kernel(const LdpcGeom& g) {
         int cnt;
         return reg_table(cnt)[g.reg_variant - 1].k[g.algo == 0 ? 0 : 1];
     }
+#if PL_DIAG
     if (g.check_kernel) return g.algo == 0 ? (void*)ldpc_check_kernel<0> : (void*)ldpc_check_kernel<1>;
+#endif
     return g.algo == 0 ? pick<0>(g.use_global) : pick<1>(g.use_global);
 }
 

@@ -860,9 +860,8 @@ struct TreeEntry {
     bool sc;
     int F, DL;
     void* fn;         // compiled for 4 waves/SIMD (<= 128 VGPRs; measured fastest)
-    void* fn_stamps;
-    void* fn_wpe1;    // compiler's own register budget (3 waves/SIMD), PL_TREE_WPE=1
-    void* fn_wpe5;    // unused (5 waves/SIMD spilled badly: 13 ms)
+    void* fn_stamps;  // PL_DIAG only: per-phase s_memtime stamps
+    void* fn_wpe1;    // PL_DIAG only: compiler's own register budget (3 waves/SIMD), PL_TREE_WPE=1
     int lds;
     int64_t ws;
 };
@@ -870,28 +869,34 @@ struct TreeEntry {
 template <int NL, int LCAP, bool SC, int F, int DL, bool VARIANTS = false, int WPE = 4>
 TreeEntry make_entry() {
     using G = TG<NL, LCAP, F, DL>;
+    void* st = nullptr;
     void* w1 = nullptr;
+#if PL_DIAG
+    st = (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, true, WPE>;
     if constexpr (VARIANTS) w1 = (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 1>;
-    return TreeEntry{NL, LCAP, SC, F, DL, (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, WPE>,
-                     (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, true, WPE>, w1, nullptr, G::LDS, G::WS};
+#endif
+    return TreeEntry{NL, LCAP, SC, F, DL, (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, WPE>, st, w1,
+                     G::LDS, G::WS};
 }
 
 // (n, list capacity) pairs built with the tree kernel: the BASELINE.json
 // configurations (N=256 SC, N=1024 SC / SCL L=8 / L=32, N=4096 SCL L=8), SCL
-// L=4/16 at N=1024, L=8 at N=2048, SC at N=256..4096, and the fused-depth
-// alternatives of the headline one (PL_TREE_F); polar_lane.hip serves every
-// other (N, L).
+// L=4/16 at N=1024, L=8 at N=2048, SC at N=256..4096; the diagnostic build adds
+// the fused-depth alternatives of the headline one and of N=4096 (PL_TREE_F).
+// polar_lane.hip serves every other (N, L).
 const TreeEntry* tree_table(int* count) {
     static const TreeEntry tab[] = {
         make_entry<10, 8, false, 3, 7, true>(),
+#if PL_DIAG
         make_entry<10, 8, false, 2, 7>(),
         make_entry<10, 8, false, 4, 7>(),
+        make_entry<12, 8, false, 3, 9>(),
+#endif
         make_entry<10, 32, false, 3, 7>(),
         make_entry<10, 16, false, 3, 7>(),
         make_entry<10, 4, false, 3, 7>(),
         make_entry<11, 8, false, 3, 8>(),
         make_entry<12, 8, false, 4, 9>(),  // N = 4096: F = 4 11.63 vs F = 3 11.89 ms (16 384 frames)
-        make_entry<12, 8, false, 3, 9>(),
         make_entry<8, 2, false, 3, 5>(),
         make_entry<8, 4, false, 3, 5>(),
         make_entry<8, 8, false, 3, 5>(),
@@ -918,14 +923,14 @@ const TreeEntry* tree_table(int* count) {
 bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info) {
     int cnt = 0;
     const TreeEntry* t = tree_table(&cnt);
-    const char* fe = std::getenv("PL_TREE_F");  // diagnostic: pick the fused-top depth
+    const char* fe = PL_DIAG ? std::getenv("PL_TREE_F") : nullptr;  // diagnostic: pick the fused-top depth
     const int want_f = fe ? std::atoi(fe) : 0;
-    const char* de = std::getenv("PL_TREE_DL");  // diagnostic: pick the first LDS depth
+    const char* de = PL_DIAG ? std::getenv("PL_TREE_DL") : nullptr;  // diagnostic: pick the first LDS depth
     const int want_dl = de ? std::atoi(de) : 0;
     for (int k = 0; k < cnt; ++k)
         if (t[k].n == n && t[k].lcap == lcap && t[k].sc == sc && (!want_f || t[k].F == want_f) &&
             (!want_dl || t[k].DL == want_dl)) {
-            const char* w = std::getenv("PL_TREE_WPE");
+            const char* w = PL_DIAG ? std::getenv("PL_TREE_WPE") : nullptr;
             const int wpe = w ? std::atoi(w) : 4;
             info->fn = (wpe == 1 && t[k].fn_wpe1) ? t[k].fn_wpe1 : t[k].fn;
             info->fn_stamps = t[k].fn_stamps;
@@ -942,8 +947,10 @@ bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info) {
 hipError_t tree_prepare(const TreeInfo& t, int* max_blocks_per_cu) {
     hipError_t e = hipFuncSetAttribute(t.fn, hipFuncAttributeMaxDynamicSharedMemorySize, t.lds_bytes);
     if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute(t.fn_stamps, hipFuncAttributeMaxDynamicSharedMemorySize, t.lds_bytes);
-    if (e != hipSuccess) return e;
+    if (t.fn_stamps) {
+        e = hipFuncSetAttribute(t.fn_stamps, hipFuncAttributeMaxDynamicSharedMemorySize, t.lds_bytes);
+        if (e != hipSuccess) return e;
+    }
     int nb = 0;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, t.fn, 64, t.lds_bytes);
     if (e != hipSuccess) return e;
@@ -956,6 +963,7 @@ hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t
                        unsigned long long* stamps, const uint32_t* crc_g, hipStream_t s) {
     void* args[] = {(void*)&llr, (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos, (void*)&batch,
                     (void*)&K, (void*)&Lsz, (void*)&ws, (void*)&stamps, (void*)&crc_g};
+    if (stamps && !t.fn_stamps) return hipErrorInvalidValue;
     return hipLaunchKernel(stamps ? t.fn_stamps : t.fn, dim3((unsigned)grid), dim3(64), args, t.lds_bytes, s);
 }
 

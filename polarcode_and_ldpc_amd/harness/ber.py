@@ -26,10 +26,24 @@ from ..utils.visualization import save_results
 from .montecarlo import MonteCarlo, PointLog, ldpc_round_fn, polar_round_fn
 
 
+def _digest(*arrays) -> str:
+    import hashlib
+    h = hashlib.sha1()
+    for a in arrays:
+        a = np.ascontiguousarray(a)
+        h.update(str(a.shape).encode())
+        h.update(a.astype(np.int64).tobytes())
+    return h.hexdigest()[:16]
+
+
 def _log(log_path, mc, **key):
+    """PointLog whose run key names everything a point's counts depend on: the
+    code construction (digest of the frozen set / H), the decoder, the frame
+    budget, the frames per round and the decoder library build."""
     if not log_path:
         return None
-    return PointLog(log_path, dict(key, round_frames=mc.batch * mc.world))
+    from .. import _native
+    return PointLog(log_path, dict(key, round_frames=mc.batch * mc.world, lib=_native.build_id()))
 
 
 def simulate_polar(snr_db_range: Sequence[float], num_frames: int, max_errors: int, config: Dict,
@@ -52,7 +66,7 @@ def simulate_polar(snr_db_range: Sequence[float], num_frames: int, max_errors: i
     mc = MonteCarlo(polar_round_fn(dec, seed=seed, crc_polynomial=crc_polynomial), info_bits=K, batch=batch,
                     group=group, device=torch.device("cuda", torch.cuda.current_device()))
     log = _log(log_path, mc, code="polar", N=N, K=K, list_size=list_size, crc=crc_polynomial, frames=num_frames,
-               max_errors=max_errors, seed=seed)
+               max_errors=max_errors, seed=seed, frozen=_digest(np.sort(np.asarray(fr))))
     pts = mc.run(snr_db_range, num_frames, max_errors, log=log)
     return np.array([p.ber for p in pts]), np.array([p.fer for p in pts]), pts
 
@@ -75,17 +89,21 @@ def simulate_ldpc(snr_db_range: Sequence[float], num_frames: int, max_errors: in
     mc = MonteCarlo(ldpc_round_fn(dec, seed=seed, info_bits=lib.k, encoder=enc), info_bits=lib.k, batch=batch,
                     group=group, device=torch.device("cuda", torch.cuda.current_device()))
     log = _log(log_path, mc, code="ldpc", n=n, k=lib.k, max_iter=dec.max_iter, random=random_codewords,
-               frames=num_frames, max_errors=max_errors, seed=seed)
+               frames=num_frames, max_errors=max_errors, seed=seed, dv=cons.get("dv", 3), dc=cons.get("dc", 6),
+               H=_digest(np.asarray(H) & 1))
     pts = mc.run(snr_db_range, num_frames, max_errors, log=log)
     return np.array([p.ber for p in pts]), np.array([p.fer for p in pts]), pts
 
 
 def run_ber_simulation(snr_db_range: np.ndarray, num_frames: int, max_errors: int, polar_config: Dict,
                        ldpc_config: Dict, output_dir: Path, use_third_party: bool = False, batch: int = 65536,
-                       list_size: int = 0, crc_polynomial: Optional[str] = None) -> Dict:
+                       list_size: int = 0, crc_polynomial: Optional[str] = None, resume: bool = False) -> Dict:
+    """ber_simulation.py:296-... -> results dict (also saved as JSON).  resume:
+    keep per-point rows in output_dir/data/ber_points.jsonl and take finished
+    points from it (opt-in: a fresh call always simulates)."""
     snr = np.asarray(snr_db_range, dtype=float)
     results = {"snr_db": snr.tolist(), "polar": {}, "ldpc": {}}
-    points = Path(output_dir) / "data" / "ber_points.jsonl"  # per-point rows: an interrupted run resumes
+    points = Path(output_dir) / "data" / "ber_points.jsonl" if resume else None
     pb, pf, pp = simulate_polar(snr, num_frames, max_errors, polar_config, list_size, crc_polynomial, batch,
                                 log_path=points)
     results["polar"]["self"] = {"ber": pb.tolist(), "fer": pf.tolist(), "points": [p.as_dict() for p in pp]}
@@ -125,17 +143,32 @@ def main(argv=None):
     ap.add_argument("--max-errors", type=int, default=100)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--log", default=None, help="JSON-lines file of finished SNR points; a rerun resumes from it")
+    ap.add_argument("--log", "--resume-log", dest="log", default=None,
+                    help="JSON-lines file of finished SNR points; a rerun resumes from it (under torchrun spell it "
+                         "--resume-log: torchrun's own parser takes --log for an abbreviation of --log-dir)")
     ap.add_argument("--ldpc-codewords", choices=["zero", "random"], default="zero",
                     help="LDPC frames: all-zero codeword, or random messages encoded on the device")
+    ap.add_argument("--cpu-stub", action="store_true",
+                    help="plumbing check on CPU: gloo ranks and a deterministic stub round function "
+                         "(montecarlo.stub_round_fn) instead of the device decoders; not a simulation")
     a = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if not a.cpu_stub:
+        torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.cpu_stub:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     snr = _parse_range(a.snr)
-    if a.code == "polar":
+    if a.cpu_stub:
+        from .montecarlo import stub_round_fn
+        mc = MonteCarlo(stub_round_fn(seed=7, info_bits=a.K), info_bits=a.K, batch=a.batch)
+        log = _log(a.log, mc, code="stub", K=a.K, frames=a.frames, max_errors=a.max_errors)
+        pts = mc.run(snr, a.frames, a.max_errors, log=log)
+        ber, fer = np.array([p.ber for p in pts]), np.array([p.fer for p in pts])
+    elif a.code == "polar":
         ber, fer, pts = simulate_polar(snr, a.frames, a.max_errors, {"encoding": {"N": a.N, "K": a.K}},
                                        a.list_size, a.crc, a.batch, log_path=a.log)
     else:

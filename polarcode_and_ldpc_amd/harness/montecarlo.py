@@ -95,6 +95,23 @@ class MonteCarlo:
         self._dist.all_reduce(t, group=self.group)
         return t.cpu().numpy()
 
+    def _finished(self, log: "Optional[PointLog]") -> dict:
+        """Finished points of `log`, read on rank 0 and broadcast, so that every
+        rank skips the same SNR points even when the ranks do not share a file
+        system (or the file changes between their reads): a disagreement would
+        pair different points' all-reduces."""
+        done = log.load() if (log is not None and self.rank == 0) else {}
+        if self.world > 1:
+            box = [sorted((k, v.as_dict()) for k, v in done.items())]
+            self._dist.broadcast_object_list(box, src=self._dist.get_global_rank(self.group, 0)
+                                             if self.group is not None else 0, group=self.group)
+            done = {}
+            for k, d in box[0]:
+                done[k] = PointResult(snr_db=d["snr_db"], frames=d["frames"], frame_errors=d["frame_errors"],
+                                      bit_errors=d["bit_errors"], info_bits=d["info_bits"],
+                                      rounds=d.get("rounds", 0)).finalize()
+        return done
+
     def run_point(self, snr_index: int, snr_db: float, num_frames: int, max_errors: int) -> PointResult:
         res = PointResult(snr_db=float(snr_db), frames=0, frame_errors=0, bit_errors=0, info_bits=self.info_bits)
         done = 0
@@ -119,7 +136,7 @@ class MonteCarlo:
         soon as it finishes (rank 0), so an interrupted sweep resumes where it
         stopped.  Point i always draws the stream (seed, i, frame): a resumed
         sweep gives the same counts as an uninterrupted one."""
-        done = log.load() if log is not None else {}
+        done = self._finished(log)
         out = []
         for i, s in enumerate(snr_db_range):
             key = round(float(s), 9)
@@ -137,8 +154,9 @@ class PointLog:
     """Append-only JSON-lines record of finished SNR points (SURVEY §5
     checkpoint / resume; the reference writes its results once at the end,
     src/utils/visualization.py:84-112).  Each row carries the run key (code,
-    decoder, frames, max_errors, frames per round, seed): rows of another
-    configuration in the same file are ignored."""
+    decoder, code construction digest, frames, max_errors, frames per round,
+    seed, decoder library build id): rows of another configuration -- or of
+    another build of the decoder library -- in the same file are ignored."""
 
     def __init__(self, path, key: dict):
         import json
@@ -273,4 +291,19 @@ def ldpc_round_fn(decoder, seed: int = 0, info_bits: Optional[int] = None, encod
             _native.count_errors(msg, out.index_select(1, info).contiguous(), k, counts)
         return counts.cpu().numpy()
 
+    return fn
+
+
+def stub_round_fn(seed: int = 0, info_bits: int = 16):
+    """Deterministic CPU round function (tests and plumbing rehearsals only): the
+    counts of frame f at SNR point i depend only on (seed, i, f), like the
+    device round functions' Philox streams, so any sharding gives the same
+    points.  Frame error iff hash(seed, i, f) % 1000 < 400 >> i; bit errors
+    1 + f % 5 per erroneous frame."""
+    def fn(snr_index, snr_db, offset, nframes):
+        f = np.arange(offset, offset + nframes, dtype=np.uint64)
+        h = (f * np.uint64(2654435761) + np.uint64((seed * 1000003 + snr_index * 97) & 0xFFFFFFFF)) % np.uint64(1000)
+        err = h < np.uint64(400 >> min(snr_index, 16))
+        bits = np.where(err, 1 + (f % np.uint64(5)), 0).astype(np.int64)
+        return np.array([int(bits.sum()), int(err.sum()), int(nframes)], dtype=np.int64)
     return fn

@@ -69,6 +69,10 @@ int main() {
     EXPECT(pl_decode_ws(nullptr, llr, 1, 8, bits, nullptr, nullptr, 0, nullptr) == PL_EINVAL);
     EXPECT(pl_plan_workspace_bytes(nullptr, 1, &ws) == PL_EINVAL);
     EXPECT(pl_plan_reserve(nullptr, 1, nullptr) == PL_EINVAL);
+    EXPECT(pl_plan_release(nullptr, nullptr) == PL_EINVAL);
+    int64_t ns = 0, nb = 0;
+    EXPECT(pl_plan_workspace_stats(nullptr, &ns, &nb) == PL_EINVAL);
+    EXPECT(pl_debug_set_plan_device(nullptr, 0) == PL_EINVAL);
     EXPECT(pl_plan_get_info(nullptr, nullptr) == PL_EINVAL);
     EXPECT(pl_plan_destroy(nullptr) == PL_OK);
     EXPECT(pl_polar_plan_set_crc(nullptr, 8, 0x1D) == PL_EINVAL);

@@ -43,16 +43,19 @@ def _host_polar(oracle, N, K, L, fr, snr, frames, seed, chunk=2048):
     return np.concatenate(per_frame)
 
 
-def _host_ldpc(oracle, H, k, snr, frames, seed, max_iter=20):
+def _host_ldpc(oracle, H, k, snr, frames, seed, max_iter=20, algo="bp", chunk=1024):
     from polarcode_and_ldpc_amd.channel import AWGNChannel
     from polarcode_and_ldpc_amd.ldpc import dense_to_csr
     np.random.seed(seed)
     ch = AWGNChannel(snr)
     n = H.shape[1]
-    llr = ch.transmit(np.zeros((frames, n), dtype=int), return_llr=True)
     rp, ci = dense_to_csr(H)
-    bits, _ = oracle.ldpc_decode(rp, ci, n, llr, "bp", max_iter, True, 1.0, threads=16)
-    return bits[:, :k].sum(axis=1)
+    per_frame = []
+    for c0 in range(0, frames, chunk):
+        llr = ch.transmit(np.zeros((min(chunk, frames - c0), n), dtype=int), return_llr=True)
+        bits, _ = oracle.ldpc_decode(rp, ci, n, llr, algo, max_iter, True, 1.0, threads=16)
+        per_frame.append(bits[:, :k].sum(axis=1))
+    return np.concatenate(per_frame)
 
 
 def _compare(dev, host_err, K, label):
@@ -89,15 +92,52 @@ def test_sc_n256_ber_fer_parity(gpu, oracle, snr):
 def test_scl_l8_n1024_ber_fer_parity(gpu, oracle, snr):
     """SCL L=8 N=1024 in its waterfall (Es/N0, the reference's SNR: FER ~6 % at
     -1.5 dB; at 0 / 1 dB FER is below 1e-3 and both sides see ~0 errors in a
-    test-sized sample)."""
+    test-sized sample).  8 192 reference-side frames per point."""
     from polarcode_and_ldpc_amd.harness.montecarlo import MonteCarlo, polar_round_fn
     from polarcode_and_ldpc_amd.polar import SCLDecoder, construct_frozen_set
     N, K, L = 1024, 512, 8
     fr = construct_frozen_set(N, K, 2.0)
     dev = MonteCarlo(polar_round_fn(SCLDecoder(N, K, L, frozen_bits=fr), seed=102), info_bits=K,
                      batch=65536).run([snr], 131072, 10 ** 12)[0]
-    host = _host_polar(oracle, N, K, L, fr, snr, 2048, seed=int(2000 + 10 * snr))
+    host = _host_polar(oracle, N, K, L, fr, snr, 8192, seed=int(2000 + 10 * snr))
     _compare(dev, host, K, "SCL L=8 N=1024 @ %g dB" % snr)
+
+
+@pytest.mark.parametrize("snr", [-2.0, -1.5, -1.0])
+def test_scl_l32_n1024_ber_fer_parity(gpu, oracle, snr):
+    """Plain SCL L=32 N=1024 (the reference's SCLDecoder at the configs[3] list
+    size; its use_crc is inert) at the low end of the configs[3] sweep.  1 536
+    reference-side frames per point (the C oracle takes ~35 ms per L=32 frame on
+    16 threads); -1 dB has FER ~0.2 %, so there both sides see only a few errors."""
+    from polarcode_and_ldpc_amd.harness.montecarlo import MonteCarlo, polar_round_fn
+    from polarcode_and_ldpc_amd.polar import SCLDecoder, construct_frozen_set
+    N, K, L = 1024, 512, 32
+    fr = construct_frozen_set(N, K, 2.0)
+    dev = MonteCarlo(polar_round_fn(SCLDecoder(N, K, L, frozen_bits=fr), seed=104), info_bits=K,
+                     batch=32768).run([snr], 65536, 10 ** 12)[0]
+    host = _host_polar(oracle, N, K, L, fr, snr, 1536, seed=int(4000 + 10 * snr), chunk=512)
+    r = _compare(dev, host, K, "SCL L=32 N=1024 @ %g dB" % snr)
+    if snr <= -1.5:
+        assert r["fer_ref"] > 0.01
+
+
+@pytest.mark.parametrize("snr", [-1.2, -1.0])
+def test_ms20_8192_ber_fer_parity(gpu, oracle, snr):
+    """Min-Sum (normalization 1.0) max_iter=20 with early stop on the n=8192
+    (3,6)-regular code of the configs[4] bench (every check degree 6: the
+    reference's MSDecoder raises on degree-1 checks), all-zero codeword, errors
+    over the first k positions; the waterfall of this code (FER ~56 % / ~5 %)."""
+    from polarcode_and_ldpc_amd.harness.montecarlo import MonteCarlo, ldpc_round_fn
+    from polarcode_and_ldpc_amd.ldpc import MSDecoder
+    from polarcode_and_ldpc_amd.ldpc.matrix import regular_construction
+    H = regular_construction(8192, 3, 6, seed=11)
+    k = 8192 - H.shape[0]
+    dec = MSDecoder(H, max_iter=20, normalization=1.0, early_stop=True)
+    dev = MonteCarlo(ldpc_round_fn(dec, seed=105, info_bits=k), info_bits=k, batch=16384).run([snr], 65536,
+                                                                                           10 ** 12)[0]
+    host = _host_ldpc(oracle, np.asarray(H), k, snr, 4096, seed=int(5000 + 10 * snr), algo="ms")
+    r = _compare(dev, host, k, "MS-20 n=8192 @ %g dB" % snr)
+    assert r["fer_ref"] > 0.01
 
 
 @pytest.mark.parametrize("snr", [-1.0, 0.5])

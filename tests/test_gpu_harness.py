@@ -138,3 +138,22 @@ def test_count_errors_vs_torch(gpu, width, ld, off):
     e = ((ref & 1) != (dec & 1)).sum(dim=1)
     want = [int(e.sum()), int((e > 0).sum()), B]
     assert counts.tolist() == want
+
+
+def test_awgn_vector_and_scalar_paths_agree(gpu):
+    """the AWGN kernel's vector path (even n and ld, 16-byte aligned
+    rows) and its scalar path (any other layout) read a codeword byte the same
+    way (bit 0) and draw the same Philox stream: an odd-pitch, offset view gets
+    exactly the LLRs of a contiguous one, also for bytes other than 0 / 1."""
+    import torch
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    B, n = 257, 64
+    g = torch.Generator().manual_seed(3)
+    cw = torch.randint(0, 256, (B, n), generator=g, dtype=torch.uint8).cuda()
+    ch = AWGNChannel(1.5)
+    a = ch.llr_batch_device(cw, n, B, seed=11, frame_offset=5)              # vector path
+    big = torch.zeros((B, n + 1), dtype=torch.float64, device="cuda")
+    b = ch.llr_batch_device(cw, n, B, seed=11, frame_offset=5, out=big[:, 1:])  # ld odd, unaligned: scalar
+    c = ch.llr_batch_device((cw & 1).contiguous(), n, B, seed=11, frame_offset=5)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(a, c)

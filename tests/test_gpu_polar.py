@@ -557,6 +557,59 @@ def test_one_plan_two_streams(gpu, N, L):
     assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
 
 
+def test_release_and_wrong_device(gpu):
+    """Boundary hardening: pl_plan_release frees a stream's
+    workspace (and the next decode regrows it with the same bits), and every
+    call on a plan from a device other than the plan's is refused with PL_EINVAL
+    (pl_debug_set_plan_device stands in for a second GPU)."""
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    P = _P()
+    N, K, L, B = 1024, 512, 8, 2048
+    fr = P.construct_frozen_set(N, K, 2.0)
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    plan = _native.polar_plan(N, K, mask, L)
+    llr = AWGNChannel(1.0).llr_batch_device(None, N, B, seed=5)
+    a = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    plan.decode(llr, a)
+    s1 = torch.cuda.Stream()
+    s1.wait_stream(torch.cuda.current_stream())
+    b = torch.zeros_like(a)
+    with torch.cuda.stream(s1):
+        plan.decode(llr, b)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    n, nbytes = plan.workspace_stats()
+    assert n == 2 and nbytes >= 2 * plan.workspace_bytes(B)
+    plan.release(s1)
+    assert plan.workspace_stats() == (1, plan.workspace_bytes(B))
+    plan.release()
+    assert plan.workspace_stats() == (0, 0)
+    plan.release()  # no workspace: no-op
+    c = torch.zeros_like(a)
+    plan.decode(llr, c)  # regrows
+    torch.cuda.synchronize()
+    assert torch.equal(a, c) and plan.workspace_stats()[0] == 1
+    plan.reserve(0)  # reserve(0) = release
+    assert plan.workspace_stats() == (0, 0)
+
+    cur = torch.cuda.current_device()
+    _native.check(_native.lib.pl_debug_set_plan_device(plan.handle, cur + 7), "set device")
+    for call in (lambda: plan.decode(llr, c), lambda: plan.reserve(B), lambda: plan.set_crc(8, 0x1D),
+                 lambda: plan.decode(llr, c, ws=torch.empty(plan.workspace_bytes(B), dtype=torch.uint8,
+                                                              device="cuda")),
+                 lambda: _native.polar_encode(plan, a, torch.empty((B, N), dtype=torch.uint8, device="cuda"))):
+        with pytest.raises(AssertionError, match="not the plan's device"):
+            call()
+    assert plan.workspace_stats() == (0, 0)  # nothing was allocated on the wrong device
+    _native.check(_native.lib.pl_debug_set_plan_device(plan.handle, cur), "set device")
+    c.zero_()
+    plan.decode(llr, c)
+    torch.cuda.synchronize()
+    assert torch.equal(a, c)
+
+
 def test_caller_workspace_and_lazy_sizing(gpu):
     """pl_decode_ws: any workspace of at least one unit decodes the same bits
     (fewer resident waves); pl_plan_workspace_bytes grows with the batch up to

@@ -56,6 +56,9 @@ namespace {
 #ifndef PL_RATE0
 #define PL_RATE0 2  // rate-0 nodes of 2..8 leaves decoded at their first leaf; >= 2: metric chains per group
 #endif
+#ifndef PL_ABL_RANK
+#define PL_ABL_RANK 0  // diagnostic ablation (PL_DIAG only): fake ranks
+#endif
 #ifndef PL_RANK_F32
 #define PL_RANK_F32 1  // strict ranks from fp32 roundings of the metrics (collisions fall back)
 #endif
@@ -420,7 +423,11 @@ PL_DEV void rate0_rest(const unsigned char* smem, const unsigned char* ws, int p
             for (int u = 0; u < IL; ++u) {
                 if (j0 + u < S) {
                     const double lam = ll[j0 + u];
+#if PL_DIAG && defined(PL_ABL_METRIC)
+                    const double t = 0.0 * lam;
+#else
                     const double t = log1p_pos(exp_neg(fabs(lam)));
+#endif
                     inc[u] = (lam >= 0.0) ? -t : lam - t;
                 }
             }
@@ -470,7 +477,13 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
     // every pruning (same rows, partial sums and bit; metric -inf), uses slot
     // 0's plane, and so loads the lines slot 0 loads and stores the values
     // slot 0 stores to the same addresses -- no memory traffic of its own.
+#if PL_DIAG && defined(PL_ABL_WSMASK)
+    // ablation timing build: every wave shares one of PL_ABL_WSMASK+1 slices, so
+    // the pools stay in L2 (wrong bits, same instruction stream)
+    unsigned char* const ws = workspace + (size_t)(blockIdx.x & PL_ABL_WSMASK) * G::WS;
+#else
     unsigned char* const ws = workspace + (size_t)blockIdx.x * G::WS;
+#endif
     uint64_t own = 0;
 #pragma unroll
     for (int d = 0; d < 12; ++d) own |= (uint64_t)slot << (RB * d);
@@ -629,7 +642,10 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     // the survivors cannot hide one below them.
                     r0 = 0;
                     r1 = 0;
-                    if constexpr (DPP) {
+                    if constexpr (PL_DIAG && PL_ABL_RANK) {
+                        r0 = 2 * slot;  // ablation timing build: no ranking (decisions change)
+                        r1 = 2 * slot + 1;
+                    } else if constexpr (DPP) {
                         const float f0 = (float)m0, f1 = (float)m1;
                         r0 = f1 > f0;  // own pair (f0 > f0 never counts)
                         r1 = f0 > f1;

@@ -15,7 +15,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-CASES = ("polar_l8", "ldpc_bp", "polar_l32", "polar_4096", "ms_8192", "polar_sc")
+CASES = ("polar_l8", "ldpc_bp", "ldpc_bp_valid", "polar_l32", "polar_4096", "ms_8192", "polar_sc")
 
 
 def worker(cases):
@@ -63,6 +63,16 @@ def worker(cases):
             out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
             ms = timeit(lambda: plan.decode(llr, out))
             res[case] = dict(ms=ms, digest=digest(out), errors=int((out != msg).any(dim=1).sum().item()))
+        elif case == "ldpc_bp_valid":
+            from polarcode_and_ldpc_amd.ldpc import BPDecoder, LDPCEncoder
+            enc = LDPCEncoder(504, 252, dv=3, dc=6, seed=42)
+            plan = BPDecoder(enc.H, max_iter=20).plan
+            B = 65536
+            llr = AWGNChannel(3.0).llr_batch_device(None, 504, B, seed=4243)
+            out = torch.empty((B, 504), dtype=torch.uint8, device="cuda")
+            its = torch.empty((B,), dtype=torch.int32, device="cuda")
+            ms = timeit(lambda: plan.decode(llr, out, its))
+            res[case] = dict(ms=ms, digest=digest(out) ^ digest(its), mean_it=float(its.double().mean().item()))
         elif case == "ldpc_bp":
             from polarcode_and_ldpc_amd.ldpc import BPDecoder, LDPCEncoder
             enc = LDPCEncoder(504, 252, dv=3, dc=6, seed=42)

@@ -326,6 +326,9 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
                 const double* hi = lo + 1;
                 const int nf = d - 1;
                 double p = 1.0;
+#if PL_DIAG && defined(PL_ABL_PROD)
+                p = lo[i == 0 ? 1 : 0];  // ablation timing build: one factor
+#else
                 int k = 0;
                 for (; k + 4 <= nf; k += 4, lo += 4, hi += 4) {
 #pragma unroll
@@ -338,10 +341,15 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
                         if (k + 2 < nf) p *= (k + 2 < i ? lo : hi)[2];
                     }
                 }
+#endif
                 // clip, 2*atanh, nan_to_num: after the clip 2*atanh is finite,
                 // so only a NaN product (NaN channel LLRs) maps to 0
                 const bool pn = __builtin_isnan(p);
+#if PL_DIAG && defined(PL_ABL_ATANH)
+                o = 2.0 * __builtin_fmax(__builtin_fmin(p, 0.999999), -0.999999);  // ablation: no atanh
+#else
                 o = two_atanh(__builtin_fmax(__builtin_fmin(p, 0.999999), -0.999999));
+#endif
                 o = pn ? 0.0 : o;
             } else {
                 o = ms_check(T + e0, i, d, g.norm);
@@ -393,7 +401,11 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
             __builtin_amdgcn_wave_barrier();
             for (int w = lane; w < wn; w += 64) {
                 const int e = wl[w];
+#if PL_DIAG && defined(PL_ABL_TANH)
+                T[e] = 0.5 * T[e];  // ablation timing build: no tanh
+#else
                 T[e] = tanh_half_clip(T[e]);
+#endif
             }
         }
         __syncthreads();  // T and the syndrome parities for the next iteration's vote / check pass

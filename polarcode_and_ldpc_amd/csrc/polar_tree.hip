@@ -59,6 +59,9 @@ namespace {
 #ifndef PL_ABL_RANK
 #define PL_ABL_RANK 0  // diagnostic ablation (PL_DIAG only): fake ranks
 #endif
+#ifndef PL_RANK_BITONIC
+#define PL_RANK_BITONIC 1  // LCAP = 32: survivors by a lane-exchange bitonic sort (collisions fall back)
+#endif
 #ifndef PL_RANK_F32
 #define PL_RANK_F32 1  // strict ranks from fp32 roundings of the metrics (collisions fall back)
 #endif
@@ -80,6 +83,69 @@ PL_DEV void group8_each(int x, Fn fn) {
     fn(dpp_i<DPP_X2>(m));
     fn(dpp_i<DPP_X1>(m));
     fn(m);
+}
+
+// ---- LCAP = 32: survivors by a bitonic sort of the frame's 64 candidate keys
+// across its 32 lanes (two keys per lane), lane exchanges by DPP / ds_swizzle
+// instead of LDS broadcasts.  Element e of lane s holds sorted position
+// 32 e + s; the network sorts descending, so lane s ends with position s --
+// survivor s -- in element 0 (model: 64-key bitonic network, 21 stages).
+// x of lane s ^ STRIDE (within the lane's 32-lane group)
+template <int STRIDE>
+PL_DEV int bit_partner(int x) {
+    if constexpr (STRIDE == 1) return dpp_i<DPP_X1>(x);
+    else if constexpr (STRIDE == 2) return dpp_i<DPP_X2>(x);
+    else if constexpr (STRIDE == 4) return dpp_i<DPP_X3>(dpp_i<DPP_MIRROR8>(x));  // (s ^ 7) ^ 3
+    else if constexpr (STRIDE == 8) return dpp_i<0x128>(x);                       // row_ror:8
+    else return __builtin_amdgcn_ds_swizzle(x, 0x401F);                           // xor 16 (32-lane groups)
+}
+constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
+// One compare-exchange stage.  Element e of lane s is position p = 32 e + s;
+// it keeps the smaller key when it is the upper element of a descending block
+// or the lower one of an ascending block (blocks of SIZE descend where p & SIZE
+// is 0; every block of the final merge descends): the same select for both
+// elements except in the SIZE = 32 merge, where element 1's block ascends.
+template <int SIZE, int STRIDE>
+PL_DEV void bit_stage(int& k0, int& k1, int s) {
+    if constexpr (STRIDE == 32) {
+        const int a = k0, b = k1;
+        k0 = a > b ? a : b;
+        k1 = a > b ? b : a;
+    } else {
+        const int p0 = bit_partner<STRIDE>(k0), p1 = bit_partner<STRIDE>(k1);
+        const int lo0 = min(k0, p0), hi0 = max(k0, p0), lo1 = min(k1, p1), hi1 = max(k1, p1);
+        const bool upper = (s & STRIDE) != 0;
+        if constexpr (SIZE == 64) {
+            k0 = upper ? lo0 : hi0;
+            k1 = upper ? lo1 : hi1;
+        } else if constexpr (SIZE == 32) {
+            k0 = upper ? lo0 : hi0;
+            k1 = upper ? hi1 : lo1;
+        } else {
+            const bool tmin = (((s >> ilog2(STRIDE)) ^ (s >> ilog2(SIZE))) & 1) == 0;
+            k0 = tmin ? lo0 : hi0;
+            k1 = tmin ? lo1 : hi1;
+        }
+    }
+}
+template <int SIZE, int STRIDE>
+PL_DEV void bit_merge(int& k0, int& k1, int s) {
+    bit_stage<SIZE, STRIDE>(k0, k1, s);
+    if constexpr (STRIDE > 1) bit_merge<SIZE, STRIDE / 2>(k0, k1, s);
+}
+template <int SIZE = 2>
+PL_DEV void bit_sort64_desc(int& k0, int& k1, int s) {
+    bit_merge<SIZE, SIZE / 2>(k0, k1, s);
+    if constexpr (SIZE < 64) bit_sort64_desc<SIZE * 2>(k0, k1, s);
+}
+// Sort key of candidate list index cidx (0..63, the reference's candidate order
+// b * nact + q up to a monotone relabelling): the fp32 rounding of its metric as
+// an order-preserving int (-0 taken as +0), low 6 bits replaced by 63 - cidx, so
+// that equal truncated metrics order by ascending list index (the stable sort).
+PL_DEV int bit_key(double m, int cidx) {
+    const int b = __float_as_int((float)m + 0.0f);
+    const int s = b ^ ((b >> 31) & 0x7FFFFFFF);
+    return (s & ~63) | (63 - cidx);
 }
 
 constexpr int RB = 5;  // bits per slot field of a pointer row (list capacity <= 32)
@@ -592,12 +658,13 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 // (a search over the 8 lanes' ranks instead of the LDS survivor
                 // table) measured slower: 6.52 ms.
                 constexpr bool DPP = F32 && LCAP == 8;
-                if constexpr (F32 && !DPP) reinterpret_cast<float2*>(met)[slot] = make_float2((float)m0, (float)m1);
+                constexpr bool BITONIC = F32 && LCAP == 32 && PL_RANK_BITONIC && !(PL_DIAG && PL_ABL_RANK);
+                if constexpr (F32 && !DPP && !BITONIC) reinterpret_cast<float2*>(met)[slot] = make_float2((float)m0, (float)m1);
                 else met[slot] = make_double2(m0, m1);
                 rowx[2 * slot] = lrow;
                 rowx[2 * slot + 1] = brow;
                 brx[slot] = (uint64_t)bb | ((uint64_t)bw5 << 32);
-                if constexpr (!DPP) lds_sync();
+                if constexpr (!DPP && !BITONIC) lds_sync();
                 // rank of (slot, b) in the stable descending order of
                 // [(m0, q) for active q] + [(m1, q) for active q]
                 constexpr int QC = LCAP < 8 ? LCAP : 8;
@@ -627,7 +694,37 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 const int tgt = slot < nsurv ? slot : 0;
                 uint32_t e = 0;  // survivor entry: parent slot << 1 | bit
                 int r0, r1;
-                if constexpr (STRICT) {
+                if constexpr (BITONIC) {
+                    // LCAP = 32: sort the 64 keys (bit_key) across the frame's
+                    // lanes; lane s then holds survivor s.  Two candidates whose
+                    // fp32 metrics agree in all but the 6 label bits at or above
+                    // the survivor boundary (or a NaN metric) send the wave to the
+                    // exact fp64 ranks below, as a tie does on the LDS path.
+                    const bool act = slot < nact;
+                    int k0 = act ? bit_key(m0, slot) : (int)0x80000000;  // (m0, slot): list index slot
+                    int k1 = act ? bit_key(m1, 32 + slot) : (int)0x80000000;  // (m1, slot): after every m0
+                    const bool bad = act && (__builtin_isnan(m0) || __builtin_isnan(m1));
+                    bit_sort64_desc(k0, k1, slot);
+                    // position s + 1: element 0 of lane s + 1, or element 1 of lane 0 for s = 31
+                    const int x = slot == 0 ? k1 : k0;
+                    const int nxt = __builtin_amdgcn_ds_bpermute((((slot + 1) & 31) + fw * 32) * 4, x);
+                    const bool lost = slot < nsurv && ((k0 ^ nxt) & ~63) == 0;
+                    const int cidx = 63 - (k0 & 63);
+                    const uint32_t eo = (uint32_t)(((cidx & 31) << 1) | (cidx >> 5));
+                    const uint32_t e0 = (uint32_t)__builtin_amdgcn_readlane((int)eo, 0);
+                    const uint32_t e32 = (uint32_t)__builtin_amdgcn_readlane((int)eo, 32);
+                    e = slot < nsurv ? eo : (fw ? e32 : e0);  // beyond the survivors: shadow survivor 0
+                    if (__ballot(lost || bad)) {
+                        lds_sync();  // the fp64 metrics of every lane
+                        exact_ranks(r0, r1);
+                        if (slot < nact) {
+                            if (r0 < nsurv) surv[r0] = id0;
+                            if (r1 < nsurv) surv[r1] = id1;
+                        }
+                        lds_sync();
+                        e = surv[tgt];
+                    }
+                } else if constexpr (STRICT) {
                     // Lists of 8+ / long codes: strict comparisons only -- exact unless two
                     // candidates tie (inactive slots publish -inf and never
                     // count).  A tie makes two candidates claim one survivor

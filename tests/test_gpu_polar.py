@@ -523,6 +523,36 @@ def test_full_batch_noisy_vs_oracle(gpu, oracle, snr):
     assert 0 < (out != msg).any(dim=1).sum().item() < B  # a noisy regime: some frames in error
 
 
+@pytest.mark.parametrize("L", [8, 32])
+def test_later_grid_passes_vs_oracle(gpu, oracle, L):
+    """The persistent grid decodes a batch in passes (grid = CUs x waves per CU
+    wavefronts, 64 / L frames each); every wavefront's later passes run on the
+    workspace and LDS its earlier frames left behind.  Frames from the last pass
+    of a noisy multi-pass batch (-2 dB) equal the oracle's, bit for bit."""
+    import torch
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    P = _P()
+    N, K = 1024, 512
+    fr = P.construct_frozen_set(N, K, 2.0)
+    dec = P.SCLDecoder(N, K, L, frozen_bits=fr)
+    per_pass = dec.plan.workspace_bytes(1 << 22) // dec.plan.workspace_bytes(64 // L) * (64 // L)
+    B = 2 * per_pass + 96  # a ragged third pass
+    msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    _native.random_bits(91, 0, msg)
+    cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+    _native.polar_encode(dec.plan, msg, cw)
+    llr = AWGNChannel(-2.0).llr_batch_device(cw, N, B, seed=92)
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    dec.plan.decode(llr, out)
+    torch.cuda.synchronize()
+    S = 256 if L == 32 else 1024
+    idx = torch.cat([torch.arange(per_pass, per_pass + S // 2), torch.arange(B - S // 2, B)]).cuda()
+    want = oracle.scl_decode(N, L, fr, llr[idx].cpu().numpy(), threads=16)
+    assert _mismatch(out[idx].cpu().numpy(), want) == 0
+    assert 0 < (out != msg).any(dim=1).sum().item() < B
+
+
 @pytest.mark.parametrize("N,L", [(1024, 8), (1024, 32), (4096, 8), (512, 4), (256, 0)])
 def test_one_plan_two_streams(gpu, N, L):
     """Plans are shared across streams (SURVEY §8 b ownership row): two batches

@@ -44,6 +44,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decoded info-Mbps: polar N=1024 SCL L=8 & LDPC(504,252) BP, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_ACHIEVABLE_GBS = 6290.0  # measured float4 copy (MI355X_MICROARCH.md, chip-level parameters)
 CLOCK_GHZ = 2.4
 
 
@@ -185,6 +186,7 @@ def roofline(name, kernel, frames, bytes_per_frame, kms):
     r["traffic_source"] = p.get("source")
     r["traffic_GBps"] = r["traffic"] / (kms / 1e3) / 1e9
     r["traffic_frac"] = r["traffic_GBps"] / HBM_PEAK_GBS
+    r["traffic_frac_of_achievable"] = r["traffic_GBps"] / HBM_ACHIEVABLE_GBS
     r["traffic_frames_profiled"] = p.get("frames")
     if "wave_time_shares" in p:
         r["wave_time_shares"] = p["wave_time_shares"]

@@ -40,6 +40,7 @@ struct pl_plan {
     int32_t* d_info_pos = nullptr;     // [K] ascending info indices
     int32_t* d_pos2info = nullptr;     // [N] index -> info rank or -1
     uint32_t* d_crc_g = nullptr;       // CA-SCL: CRC contribution of x_hat bit j [N] (null = plain SCL)
+    uint32_t* d_r0k = nullptr;         // SC tree kernel: log2 size of the largest all-frozen node at leaf i (4-bit fields)
     std::vector<int32_t> h_info;       // ascending info positions (host copy)
     bool tree = false;      // compile-time-geometry kernel (polar_tree.hip); else polar_lane.hip
     pl::TreeInfo tinfo{};
@@ -154,6 +155,27 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
     }
     p->pg.N = N;
     p->pg.K = K;
+    if (p->tree && p->sc) {
+        // r0k[i] (decode order): the largest k with i a multiple of 2^k (any k
+        // for i = 0) and leaves i .. i + 2^k - 1 all frozen.  K >= 1 info bits,
+        // so k < n <= 15: eight 4-bit fields per word, which the kernel reads
+        // with scalar loads.
+        std::vector<uint32_t> r0k((size_t)(N + 7) / 8, 0u);
+        for (int i = 0; i < N; ++i) {
+            int k = 0;
+            while (k + 1 < n + 1 && (i & ((1 << (k + 1)) - 1)) == 0 && i + (1 << (k + 1)) <= N) {
+                bool all = true;
+                for (int t = i; t < i + (1 << (k + 1)) && all; ++t) all = (fdec[t >> 5] >> (t & 31)) & 1u;
+                if (!all) break;
+                ++k;
+            }
+            r0k[(size_t)i >> 3] |= (uint32_t)k << (4 * (i & 7));
+        }
+        if ((e = upload(&p->d_r0k, r0k)) != hipSuccess) {
+            pl_plan_destroy(p);
+            return hipfail(e, "plan upload");
+        }
+    }
     int per_cu = 1;
     if (p->tree) {
         p->pg.F = p->tinfo.F;
@@ -345,7 +367,7 @@ static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld,
         hipError_t e;
         if (p->tree)
             e = pl::tree_launch(p->tinfo, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, p->pg.K,
-                                p->sc ? 1 : p->list_size, (unsigned char*)ws, grid, stamps, p->d_crc_g, s);
+                                p->sc ? 1 : p->list_size, (unsigned char*)ws, grid, stamps, p->d_crc_g, p->d_r0k, s);
         else if (stamps)
             return fail(PL_EUNSUPPORTED, "stamps only for the tree kernel");
         else
@@ -573,6 +595,7 @@ extern "C" int pl_plan_destroy(pl_plan* p) {
     if (p->d_info_pos) hipFree(p->d_info_pos);
     if (p->d_pos2info) hipFree(p->d_pos2info);
     if (p->d_crc_g) hipFree(p->d_crc_g);
+    if (p->d_r0k) hipFree(p->d_r0k);
     if (p->d_ldpc) hipFree(p->d_ldpc);
     p->ws.clear();  // each Workspace frees its buffer (hipFree waits for work that still uses it)
     delete p;

@@ -47,7 +47,7 @@ bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info);
 hipError_t tree_prepare(const TreeInfo& t, int* max_blocks_per_cu);
 hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t* out, const uint32_t* frozen_dec,
                        const int32_t* info_pos, int64_t batch, int K, int Lsz, unsigned char* ws, int grid,
-                       unsigned long long* stamps, const uint32_t* crc_g, hipStream_t s);
+                       unsigned long long* stamps, const uint32_t* crc_g, const uint32_t* r0k, hipStream_t s);
 
 
 hipError_t polar_encode_launch(int N, int K, const int32_t* pos2info, const uint8_t* msg,

@@ -242,6 +242,9 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
 // tid + j*256 (j < VPT); their edge metadata, var_edge / var_chk lists and
 // channel LLRs are loaded once into registers instead of once per iteration.
 // Same passes, barriers and arithmetic as ldpc_decode_kernel (bit-identical).
+#ifndef PL_MS_REGIDX
+#define PL_MS_REGIDX 1  // regular min-sum codes: adjacency indices cached in registers
+#endif
 #ifndef PL_LDPC_REG_WPE
 #define PL_LDPC_REG_WPE 4  // waves per SIMD the register budget is built for
 #endif
@@ -494,11 +497,41 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
         for (int j = 0; j < VPT; ++j) chv[j] = tid + 1024 * j < n ? ch[tid + 1024 * j] : 0.0;
     }
     for (int v = tid; v < n; v += nt) tot[v] = ch[v];
+    // Regular codes (the BASELINE n = 8192 one): every adjacency index this
+    // thread uses -- the DC columns of its checks tid + 1024 q and the DV
+    // (check << 4 | position) entries of its variables -- packed two per
+    // register, loaded once instead of from L2 every iteration (n <= 65536).
+    constexpr bool RI = (PL_MS_REGIDX & 1) && DV > 0 && DC > 0 && VPT > 0 && (DC % 2) == 0;
+    constexpr int MQ = RI ? (VPT * DV + DC - 1) / DC : 1;  // checks per thread (m = n DV / DC)
+    uint32_t ccol[RI ? MQ : 1][RI ? DC / 2 : 1];
+    constexpr bool RV = RI && (PL_MS_REGIDX & 2);
+    uint32_t vcp[RV ? VPT : 1][RV ? (DV + 1) / 2 : 1];
+    if constexpr (RI) {
+#pragma unroll
+        for (int q = 0; q < MQ; ++q) {
+            const int c = tid + 1024 * q;
+#pragma unroll
+            for (int k = 0; k < DC / 2; ++k)
+                ccol[q][k] = c < m ? ((uint32_t)ci[c * DC + 2 * k] | ((uint32_t)ci[c * DC + 2 * k + 1] << 16)) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < (RV ? VPT : 0); ++j) {
+            const int v = tid + 1024 * j;
+#pragma unroll
+            for (int k = 0; k < (DV + 1) / 2; ++k) {
+                const uint32_t lo = v < n ? (uint32_t)dv.var_cp[v * DV + 2 * k] : 0u;
+                const uint32_t hi = (v < n && 2 * k + 1 < DV) ? (uint32_t)dv.var_cp[v * DV + 2 * k + 1] : 0u;
+                vcp[j][k] = lo | (hi << 16);
+            }
+        }
+    }
     __syncthreads();
     int done = g.max_iter;
     for (int it = 0; it < g.max_iter; ++it) {
         int syn = 0;
-        for (int c = tid; c < m; c += nt) {
+#pragma unroll
+        for (int q = 0; q < (RI ? MQ : 1); ++q)
+        for (int c = tid + 1024 * q; c < m; c += (RI ? m : nt)) {
             const int e0 = DC > 0 ? c * DC : rp[c], d = DC > 0 ? DC : rp[c + 1] - e0;
             const double2 om = smin[c];
             const uint32_t ometa = smeta[c];
@@ -506,7 +539,10 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
             uint32_t idx1 = 0, ncnt = 0, nidx = 0, zcnt = 0, zidx = 0, par = 0, negs = 0;
             int s = 0;
             int cidx[DC > 0 ? DC : 1];
-            if constexpr (DC > 0) {
+            if constexpr (RI) {
+#pragma unroll
+                for (int k = 0; k < DC; ++k) cidx[k] = (int)((ccol[q][k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+            } else if constexpr (DC > 0) {
 #pragma unroll
                 for (int k = 0; k < DC; ++k) cidx[k] = ci[e0 + k];
             }
@@ -551,7 +587,8 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
             if constexpr (DV > 0 && DV < 8) {  // sequential np.sum, loads issued together
                 int cpk[DV];
 #pragma unroll
-                for (int k = 0; k < DV; ++k) cpk[k] = cp[k];
+                for (int k = 0; k < DV; ++k)
+                    cpk[k] = RV ? (int)((vcp[RV ? jv : 0][k >> 1] >> (16 * (k & 1))) & 0xFFFFu) : cp[k];
                 sum = 0.0;
 #pragma unroll
                 for (int k = 0; k < DV; ++k)

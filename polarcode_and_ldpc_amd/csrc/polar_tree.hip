@@ -530,7 +530,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restrict__ out,
                   const uint32_t* __restrict__ frozen_dec, const int32_t* __restrict__ info_pos, int64_t batch,
                   int K, int Lsz, unsigned char* __restrict__ workspace, unsigned long long* __restrict__ stamps,
-                  const uint32_t* __restrict__ crc_g) {
+                  const uint32_t* __restrict__ crc_g, const uint32_t* __restrict__ r0k) {
     using G = TG<NL, LCAP, F, DL>;
     constexpr int n = G::n, N = G::N, FPW = G::FPW;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -612,26 +612,38 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         int nact = 1;
         int root_par = 0;
         STAMP(7);
+        int nextK = (SC && r0k) ? (int)(r0k[0] & 15u) : 0;  // SC: r0k of the next leaf (scalar load, a leaf ahead)
 
         for (int i = 0; i < N; ++i) {
             // ================================================ LLRs down to leaf i
             const int dstart = (i == 0) ? 1 : n - __builtin_ctz(i);
             const int pslot = (!G::SHADOW || slot < nact) ? slot : 0;  // shadows use slot 0's planes
             const int plane = G::pl(pslot, fw);
-            double lam;
-            if (dstart <= DL) ws_sync();  // workspace written by other lanes
-            STAMP(7);
-            if (dstart <= F) {
-                lam = descend_fused<G>(smem, ws, lane, fw, plane, i, ch, raw, brow, bb, bw5);
-                lrow = set_range(lrow, (!G::SHADOW || slot < nact) ? own : 0ull, F, n);
-                STAMP(0);
-            } else {
-                const int p = dstart - 1;
-                const int ps = G::pl(field(lrow, p), fw);
-                const int bs = G::pl(field(brow, dstart <= G::NB ? dstart : 0), fw);
-                lam = descend_from<G, F>(p, smem, ws, plane, ps, bs, bb, bw5);
-                lrow = set_range(lrow, (!G::SHADOW || slot < nact) ? own : 0ull, dstart, n);
-                if (p < DL) { STAMP(1); } else { STAMP(2); }
+            // SC: leaves i .. i + 2^skipK - 1 form the largest all-frozen node
+            // that starts at leaf i (host table, decode order).  SC decides a
+            // frozen bit without its LLR and nothing inside the node is read
+            // after it, so those leaves are not decoded at all: the descent to
+            // leaf i is skipped when every array it would store lies inside the
+            // node (skipK = ctz i), and otherwise runs only for the ancestors'
+            // arrays it stores on the way; the node's partial sums are zeros.
+            const int skipK = SC ? nextK : 0;
+            const bool skip_descend = SC && skipK > 0 && i > 0 && skipK >= __builtin_ctz(i);
+            double lam = 0.0;
+            if (!skip_descend) {
+                if (dstart <= DL) ws_sync();  // workspace written by other lanes
+                STAMP(7);
+                if (dstart <= F) {
+                    lam = descend_fused<G>(smem, ws, lane, fw, plane, i, ch, raw, brow, bb, bw5);
+                    lrow = set_range(lrow, (!G::SHADOW || slot < nact) ? own : 0ull, F, n);
+                    STAMP(0);
+                } else {
+                    const int p = dstart - 1;
+                    const int ps = G::pl(field(lrow, p), fw);
+                    const int bs = G::pl(field(brow, dstart <= G::NB ? dstart : 0), fw);
+                    lam = descend_from<G, F>(p, smem, ws, plane, ps, bs, bb, bw5);
+                    lrow = set_range(lrow, (!G::SHADOW || slot < nact) ? own : 0ull, dstart, n);
+                    if (p < DL) { STAMP(1); } else { STAMP(2); }
+                }
             }
 
             // ================================================ decision at leaf i
@@ -839,7 +851,10 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
             // the descent to leaf i) without a descent each; the metrics are
             // added in leaf order.  Same operations on the same operands as the
             // leaf-by-leaf schedule.
-            if constexpr (PL_RATE0 != 0) {
+            if constexpr (SC) {
+                if (skipK > 0) i += (1 << skipK) - 1;  // the walk below runs for the node's last leaf
+                nextK = (r0k && i + 1 < N) ? (int)((r0k[(i + 1) >> 3] >> (4 * ((i + 1) & 7))) & 15u) : 0;
+            } else if constexpr (PL_RATE0 != 0) {
                 if (frozen) {
                     const int k = rate0_k(frozen_dec, i);
                     if (k > 0) {
@@ -859,16 +874,29 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
             {
                 const int to = __builtin_ctz(~(unsigned)i);
                 const int steps = to < n ? to : n;
-                int dd = n;
+                // SC, skipped node of 2^skipK leaves: the walk starts at the node's
+                // own depth with its 2^skipK zero partial sums (skipK <= steps)
+                int dd = n - skipK;
                 uint32_t cur = (uint32_t)bit;
-                int k = 0;
+                int k = skipK;
+                if (SC && skipK > 5 && k == steps) {
+                    // the node is a left child at a multi-word depth: store its
+                    // zero words as that depth's partial sums (read by the right
+                    // sibling's g), nothing to combine
+                    uint32_t* dst = reinterpret_cast<uint32_t*>(ws + G::bl_off(dd)) + G::pl(slot, fw);
+                    for (int w = 0; w < (1 << (skipK - 5)); ++w) dst[w * 64] = 0u;
+                    brow = set_field(brow, dd, slot);
+                    k = steps + 1;  // done (no register store either)
+                }
                 for (; k < steps && k < 5; ++k) {
                     const uint32_t left = beta_get<n>(dd, bb, bw5);
                     const uint32_t msk = (1u << (1 << k)) - 1u;
                     cur = spread16((left ^ cur) & msk) | (spread16(cur & msk) << 1);
                     --dd;
                 }
-                if (k == steps) {
+                if (k > steps) {
+                    // SC skipped node stored above
+                } else if (k == steps) {
                     beta_set<n>(dd, cur, bb, bw5);  // dd >= n-5: a left child, kept in registers
                 } else {
                     // dd == n-5, cur = one word: multi-word combine through the workspace.
@@ -879,6 +907,9 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     int parity = 0;
                     ws_sync();  // multi-word betas of other lanes live in the workspace
                     walkw[0] = cur;
+                    if (SC && skipK > 5) {  // the skipped node's zero words (k = skipK)
+                        for (int w = 1; w < (1 << (skipK - 5)); ++w) walkw[w * 64] = 0u;
+                    }
                     for (; k < steps; ++k) {
                         const int cwc = 1 << (k - 5);
                         const int ls = G::pl(field(brow, dd <= G::NB ? dd : 0), fw);
@@ -1073,9 +1104,9 @@ hipError_t tree_prepare(const TreeInfo& t, int* max_blocks_per_cu) {
 
 hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t* out, const uint32_t* frozen_dec,
                        const int32_t* info_pos, int64_t batch, int K, int Lsz, unsigned char* ws, int grid,
-                       unsigned long long* stamps, const uint32_t* crc_g, hipStream_t s) {
+                       unsigned long long* stamps, const uint32_t* crc_g, const uint32_t* r0k, hipStream_t s) {
     void* args[] = {(void*)&llr, (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos, (void*)&batch,
-                    (void*)&K, (void*)&Lsz, (void*)&ws, (void*)&stamps, (void*)&crc_g};
+                    (void*)&K, (void*)&Lsz, (void*)&ws, (void*)&stamps, (void*)&crc_g, (void*)&r0k};
     if (stamps && !t.fn_stamps) return hipErrorInvalidValue;
     return hipLaunchKernel(stamps ? t.fn_stamps : t.fn, dim3((unsigned)grid), dim3(64), args, t.lds_bytes, s);
 }

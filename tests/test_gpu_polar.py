@@ -748,3 +748,48 @@ def test_random_frozen_sets_rate0_nodes(gpu, oracle, N, L, K):
         want = oracle.scl_decode(N, L, fr, llr, threads=8)
         got = P.SCLDecoder(N, K, list_size=L, frozen_bits=fr).decode_batch(llr)
     assert _mismatch(got, want) == 0
+
+
+def _block_frozen_set(N, rng):
+    """A frozen set made of aligned all-frozen blocks in DECODE order (leaf i
+    decodes index bitrev(i)): nodes of every size from 2 to N/2, at random
+    positions, plus scattered single frozen leaves -- the SC kernel's rate-0
+    skip meets nodes at register depths, at the multi-word depths (>= 64
+    leaves), as left and as right children, and at the frame's start."""
+    n = N.bit_length() - 1
+    m = np.zeros(N, bool)
+    for _ in range(rng.randint(2, 8)):
+        k = rng.randint(1, n)
+        start = rng.randint(0, N >> k) << k
+        m[start:start + (1 << k)] = True
+    m |= rng.rand(N) < 0.15
+    if rng.rand() < 0.5:
+        m[:1 << rng.randint(3, n)] = True  # a frozen prefix node
+    if m.all():
+        m[-1] = False
+    rev = np.array([int(format(i, "0%db" % n)[::-1], 2) for i in range(N)])
+    return np.sort(rev[np.nonzero(m)[0]])
+
+
+@pytest.mark.parametrize("N", [128, 256, 512, 1024, 2048, 4096])
+def test_sc_rate0_node_skip_vs_oracle(gpu, oracle, N, monkeypatch):
+    """SC skips every all-frozen node (any size) without decoding its leaves:
+    random block-structured frozen sets, noisy frames, a persistent grid forced
+    to a few waves so each wavefront decodes several passes of 64 frames over
+    stale workspace (PL_POLAR_WAVES): bits equal the oracle's."""
+    P = _P()
+    rng = np.random.RandomState(N + 11)
+    monkeypatch.setenv("PL_POLAR_WAVES", "3")
+    for trial in range(3):
+        fr = _block_frozen_set(N, rng)
+        K = N - len(fr)
+        enc = P.PolarEncoder(N, K, frozen_bits=fr)
+        B = 3 * 64 * 2 + 37
+        msg = rng.randint(0, 2, (B, K))
+        snr = rng.uniform(-1.0, 3.0, size=(B, 1))
+        sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+        llr = 2.0 * ((1.0 - 2.0 * enc.encode_batch(msg)) + sigma * rng.randn(B, N)) / sigma ** 2
+        dec = P.SCDecoder(N, K, frozen_bits=fr)
+        assert dec.plan.info.reserved == 4  # the tree kernel
+        got = dec.decode_batch(llr)
+        assert _mismatch(got, oracle.sc_decode(N, fr, llr, threads=8)) == 0, (trial, K)

@@ -15,7 +15,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-CASES = ("polar_l8", "ldpc_bp", "ldpc_bp_valid", "polar_l32", "polar_4096", "ms_8192", "polar_sc")
+CASES = ("polar_l8", "ldpc_bp", "ldpc_bp_valid", "polar_l32", "polar_4096", "ms_8192", "polar_sc", "polar_sc_def",
+         "polar_sc256")
 
 
 def worker(cases):
@@ -49,9 +50,14 @@ def worker(cases):
     for case in cases:
         if case.startswith("polar"):
             N, L, B, snr = {"polar_l8": (1024, 8, 65536, 3.0), "polar_l32": (1024, 32, 16384, 1.0),
-                            "polar_4096": (4096, 8, 16384, 1.0), "polar_sc": (1024, 0, 65536, 3.0)}[case]
+                            "polar_4096": (4096, 8, 16384, 1.0), "polar_sc": (1024, 0, 65536, 3.0),
+                            "polar_sc_def": (1024, 0, 65536, 3.0), "polar_sc256": (256, 0, 65536, 3.0)}[case]
             K = N // 2
-            fr = construct_frozen_set(N, K, 2.0)
+            if case == "polar_sc_def":  # the reference's default set (generate_frozen_bits)
+                from polarcode_and_ldpc_amd.polar import SCDecoder
+                fr = SCDecoder(N, K).frozen_bits
+            else:
+                fr = construct_frozen_set(N, K, 2.0)
             mask = np.zeros(N, np.uint8)
             mask[fr] = 1
             plan = _native.polar_plan(N, K, mask, L)
@@ -91,7 +97,7 @@ def worker(cases):
             H = regular_construction(8192, 3, 6, seed=11)
             plan = MSDecoder(H, max_iter=20, early_stop=False).plan
             B = 16384
-            llr = AWGNChannel(1.5).llr_batch_device(None, 8192, B, seed=46)
+            llr = AWGNChannel(1.0).llr_batch_device(None, 8192, B, seed=46)  # many frames fail: nonzero bits
             out = torch.empty((B, 8192), dtype=torch.uint8, device="cuda")
             its = torch.empty((B,), dtype=torch.int32, device="cuda")
             ms = timeit(lambda: plan.decode(llr, out, its))

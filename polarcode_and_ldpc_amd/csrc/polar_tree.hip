@@ -1025,8 +1025,8 @@ TreeEntry make_entry() {
 
 // (n, list capacity) pairs built with the tree kernel: the BASELINE.json
 // configurations (N=256 SC, N=1024 SC / SCL L=8 / L=32, N=4096 SCL L=8), SCL
-// L=4/16 at N=1024, L=8 at N=2048, SC at N=256..4096; the diagnostic build adds
-// the fused-depth alternatives of the headline one and of N=4096 (PL_TREE_F).
+// L=4/16 at N=1024, L=8 at N=2048, SC at N=128..4096; the diagnostic build adds
+// the tier alternatives measured against them (PL_TREE_F, PL_TREE_DL, PL_TREE_DLOFF).
 // polar_lane.hip serves every other (N, L).
 const TreeEntry* tree_table(int* count) {
     static const TreeEntry tab[] = {
@@ -1051,12 +1051,24 @@ const TreeEntry* tree_table(int* count) {
         make_entry<10, 2, false, 3, 7>(),
         make_entry<7, 8, false, 3, 4>(),
         make_entry<7, 32, false, 3, 4>(),
-        make_entry<7, 1, true, 3, 4>(),
-        make_entry<8, 1, true, 3, 5>(),
-        make_entry<9, 1, true, 3, 6>(),
+        // SC: no fused top (a lane's frame shares its channel row with no other
+        // lane) and five LDS depths (62 doubles per frame, 31 KB per wave, 5
+        // waves per CU): N=1024 1.88 -> 1.28 ms, N=4096 5.78 -> 4.47 ms against
+        // F = 3, DL = n-3 (profiles/r03_d/ab_sc_tiers.log)
+        make_entry<7, 1, true, 1, 2>(),
+        make_entry<8, 1, true, 1, 3>(),
+        make_entry<9, 1, true, 1, 4>(),
+        make_entry<10, 1, true, 1, 5>(),
+        make_entry<11, 1, true, 1, 6>(),
+        make_entry<12, 1, true, 1, 7>(),
+#if PL_DIAG  // after the product entries: picked only through PL_TREE_F / PL_TREE_DL(OFF)
+        make_entry<10, 32, false, 4, 7>(),
+        make_entry<10, 32, false, 2, 7>(),
         make_entry<10, 1, true, 3, 7>(),
-        make_entry<11, 1, true, 3, 8>(),
-        make_entry<12, 1, true, 3, 9>(),
+        make_entry<10, 1, true, 2, 7>(),
+        make_entry<10, 1, true, 1, 6>(),
+        make_entry<10, 1, true, 1, 4>(),
+#endif
     };
     *count = (int)(sizeof(tab) / sizeof(tab[0]));
     return tab;
@@ -1070,7 +1082,8 @@ bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info) {
     const char* fe = PL_DIAG ? std::getenv("PL_TREE_F") : nullptr;  // diagnostic: pick the fused-top depth
     const int want_f = fe ? std::atoi(fe) : 0;
     const char* de = PL_DIAG ? std::getenv("PL_TREE_DL") : nullptr;  // diagnostic: pick the first LDS depth
-    const int want_dl = de ? std::atoi(de) : 0;
+    const char* doff = PL_DIAG ? std::getenv("PL_TREE_DLOFF") : nullptr;  // diagnostic: first LDS depth n - value
+    const int want_dl = de ? std::atoi(de) : (doff ? n - std::atoi(doff) : 0);
     for (int k = 0; k < cnt; ++k)
         if (t[k].n == n && t[k].lcap == lcap && t[k].sc == sc && (!want_f || t[k].F == want_f) &&
             (!want_dl || t[k].DL == want_dl)) {

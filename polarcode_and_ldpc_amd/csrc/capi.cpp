@@ -125,7 +125,7 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
         return fail(PL_EINVAL, "N must be a power of 2 in [2, 32768]");
     if (!(0 < K && K <= N)) return fail(PL_EINVAL, "K (info positions) must be in [1, N]");
     if (list_size < 0) return fail(PL_EINVAL, "list_size must be >= 1 (0 = SC)");
-    if (list_size > 256) return fail(PL_EUNSUPPORTED, "list_size > 256 not supported by this build (8-bit path slots)");
+    if (list_size > 1024) return fail(PL_EUNSUPPORTED, "list_size > 1024 not supported by this build (one workgroup per frame)");
     if (!frozen_mask) return fail(PL_EINVAL, "frozen_mask is NULL");
     int n = 0;
     while ((1 << n) < N) ++n;

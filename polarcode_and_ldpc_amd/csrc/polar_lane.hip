@@ -32,7 +32,7 @@ int lane_geom(int N, int K, int list_size, int F, int lds_budget, LaneGeom* g) {
     }
     g->lds_final = lds; lds += fpw * g->cw * 4;
     lds = (lds + 15) & ~15;
-    if (lcap > 64) { g->lds_xchg = lds; lds += lw * (16 + 32 + 8); }
+    if (lcap > 64) { g->lds_xchg = lds; lds += lw * (16 + (lcap > 256 ? 64 : 32) + 8); }  // (m0, m1), pointer row, ranks
     int Dl = g->D + 1;
     if (g->B > 0) {
         // deepest depths first, while they fit the LDS budget
@@ -66,7 +66,9 @@ static void* lane_kernel(const LaneGeom& g, bool sc) {
         case 32: return lane_pick_mid(g.lcap, g.F, g.B);
         case 64:   // one frame per wave
         case 128:  // one frame per workgroup of 2 waves
-        case 256: return lane_pick_large(g.lcap, g.F, g.B);  // 4 waves
+        case 256:                                             // 4 waves
+        case 512:                                             // 8 waves (16-bit row fields)
+        case 1024: return lane_pick_large(g.lcap, g.F, g.B);  // 16 waves
         default: return nullptr;
     }
 }

@@ -1,6 +1,6 @@
 // polar_lane.hpp -- the lane-per-path kernel template (see the comment below);
 // instantiated in polar_lane.hip (SC, lists 1..8), polar_lane_mid.hip (16, 32)
-// and polar_lane_big.hip (64..256) so the three compile in parallel.
+// and polar_lane_big.hip (64..1024) so the three compile in parallel.
 // Batched polar SC / SCL decoder for gfx950 (MI355X) -- lane-per-path kernel.
 //
 // Semantics: src/polar/decoder.py of the reference --
@@ -20,7 +20,7 @@
 //   * all tree arrays are lane-interleaved ([element][64 lanes]): the 64 lanes
 //     touch 64 consecutive doubles -> conflict-free LDS / coalesced global;
 //   * LLR arrays are pooled per depth with per-path slot pointers: a clone copies
-//     a 32-byte pointer row (ds_bpermute), never data.  A path only writes depths
+//     a 32-byte pointer row (64-byte above 256 paths; ds_bpermute or LDS), never data.  A path only writes depths
 //     whose previous contents are dead for every path of its frame;
 //   * depth tiers: the top F depths are recomputed from the channel LLRs, depths
 //     [F, Dl) live in a per-wave global workspace (L2/MALL resident), depths
@@ -42,29 +42,50 @@ namespace pl {
 
 namespace {
 
-struct Row {  // byte d of (a0|a1): LLR slot of depth d; byte d of (b0|b1): beta slot of depth d
-    uint64_t a0, a1, b0, b1;
+// Pointer row of a path: field d of a[] = LLR pool slot of depth d, field d of
+// b[] = beta slot of depth d (depths 0..kMaxDepth).  FB bits per field: 8 for
+// lists up to 256, 16 above.
+template <int FB>
+struct RowT {
+    static constexpr int PW = 64 / FB;                       // fields per word
+    static constexpr int NW = (kMaxDepth + 1 + PW - 1) / PW;  // words per kind
+    static constexpr uint64_t M = (1ull << FB) - 1ull;
+    static constexpr uint64_t REP = FB == 8 ? 0x0101010101010101ull : 0x0001000100010001ull;
+    uint64_t a[NW], b[NW];
 };
-PL_DEV int row_llr(const Row& r, int d) {
-    const uint64_t w = (d < 8) ? r.a0 : r.a1;
-    return (int)((w >> ((d & 7) * 8)) & 0xFFu);
+template <class R>
+PL_DEV uint64_t row_word(const uint64_t* w, int d) {  // the word holding field d (selects, no dynamic index)
+    uint64_t x = w[0];
+#pragma unroll
+    for (int k = 1; k < R::NW; ++k) x = d >= k * R::PW ? w[k] : x;
+    return x;
 }
-PL_DEV int row_beta(const Row& r, int d) {
-    const uint64_t w = (d < 8) ? r.b0 : r.b1;
-    return (int)((w >> ((d & 7) * 8)) & 0xFFu);
+template <class R>
+PL_DEV int row_llr(const R& r, int d) {
+    return (int)((row_word<R>(r.a, d) >> ((d % R::PW) * (64 / R::PW))) & R::M);
 }
-PL_DEV uint64_t byte_range_mask(int a, int b) {
+template <class R>
+PL_DEV int row_beta(const R& r, int d) {
+    return (int)((row_word<R>(r.b, d) >> ((d % R::PW) * (64 / R::PW))) & R::M);
+}
+template <class R>
+PL_DEV uint64_t field_range_mask(int a, int b) {  // fields [a, b) of one word
+    constexpr int FB = 64 / R::PW;
+    a = a < 0 ? 0 : (a > R::PW ? R::PW : a);
+    b = b < 0 ? 0 : (b > R::PW ? R::PW : b);
     if (b <= a) return 0ull;
-    const uint64_t hi = (b >= 8) ? ~0ull : ((1ull << (8 * b)) - 1ull);
-    const uint64_t lo = (a <= 0) ? 0ull : ((1ull << (8 * a)) - 1ull);
+    const uint64_t hi = (b >= R::PW) ? ~0ull : ((1ull << (FB * b)) - 1ull);
+    const uint64_t lo = (a <= 0) ? 0ull : ((1ull << (FB * a)) - 1ull);
     return hi & ~lo;
 }
-PL_DEV int clamp8(int x) { return x < 0 ? 0 : (x > 8 ? 8 : x); }
-PL_DEV void fill_pair(uint64_t& w0, uint64_t& w1, int lo, int hi, int val) {  // depths [lo, hi) := val
-    const uint64_t rep = (uint64_t)(uint32_t)val * 0x0101010101010101ull;
-    const uint64_t m0 = byte_range_mask(clamp8(lo), clamp8(hi)), m1 = byte_range_mask(clamp8(lo - 8), clamp8(hi - 8));
-    w0 = (w0 & ~m0) | (rep & m0);
-    w1 = (w1 & ~m1) | (rep & m1);
+template <class R>
+PL_DEV void fill_fields(uint64_t* w, int lo, int hi, int val) {  // depths [lo, hi) := val
+    const uint64_t rep = (uint64_t)(uint32_t)val * R::REP;
+#pragma unroll
+    for (int k = 0; k < R::NW; ++k) {
+        const uint64_t m = field_range_mask<R>(lo - k * R::PW, hi - k * R::PW);
+        w[k] = (w[k] & ~m) | (rep & m);
+    }
 }
 PL_DEV uint32_t bperm(int src_lane, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
@@ -148,8 +169,8 @@ PL_DEV void level_any(const Ctx& c, int cd, bool right, int ps, int bs, int os) 
 }
 
 // depth-F node for leaf i straight from the channel (depths 1..F recomputed)
-template <int F>
-PL_DEV double fused_top(const Ctx& c, int i, const double* __restrict__ ch, const Row& row, int os) {
+template <int F, class R>
+PL_DEV double fused_top(const Ctx& c, int i, const double* __restrict__ ch, const R& row, int os) {
     const LaneGeom& g = *c.g;
     const int n = g.n;
     const int S = 1 << (n - F);
@@ -194,6 +215,7 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int FPW = LCAP >= 64 ? 1 : 64 / LCAP;
     constexpr int LW = LCAP > 64 ? LCAP : 64;  // lanes per workgroup
+    using Row = RowT<(LCAP > 256 ? 16 : 8)>;
     const int lane = threadIdx.x;
     const int fw = lane / LCAP, slot = lane % LCAP;
     const int n = g.n, N = g.N;
@@ -211,7 +233,8 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
         const bool live = frame < batch;
         const double* __restrict__ ch = llr + (live ? frame : batch - 1) * ld;
         Row row;
-        row.a0 = row.a1 = row.b0 = row.b1 = (uint64_t)(uint32_t)slot * 0x0101010101010101ull;
+#pragma unroll
+        for (int k = 0; k < Row::NW; ++k) row.a[k] = row.b[k] = (uint64_t)(uint32_t)slot * Row::REP;
         double pm = (slot == 0) ? 0.0 : -INFINITY;
         int nact = 1;
         int root_par = 0;
@@ -221,14 +244,14 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
             const int dstart = (i == 0) ? 1 : n - __builtin_ctz(i);
             double lam;
             if (B == 0) {
-                lam = fused_top<F>(c, i, ch, row, lane);  // F == n
+                lam = fused_top<F, Row>(c, i, ch, row, lane);  // F == n
             } else {
                 int src;
                 if (dstart <= D) {
                     int d;
                     if (dstart < c.g->Dl) __syncthreads();  // workspace written by other lanes: vmcnt(0)
                     if (dstart <= F) {
-                        fused_top<F>(c, i, ch, row, lane);
+                        fused_top<F, Row>(c, i, ch, row, lane);
                         d = F;
                     } else {
                         level_any(c, dstart, true, c.base + row_llr(row, dstart - 1), c.base + row_beta(row, dstart),
@@ -236,7 +259,7 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                         d = dstart;
                     }
                     for (; d < D; ++d) level_any(c, d + 1, false, lane, lane, lane);
-                    fill_pair(row.a0, row.a1, dstart > F ? dstart : F, D + 1, slot);
+                    fill_fields<Row>(row.a, dstart > F ? dstart : F, D + 1, slot);
                     src = lane;
                 } else {
                     src = c.base + row_llr(row, D);
@@ -278,10 +301,14 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                 // the candidate this slot receives
                 double2* const xm = reinterpret_cast<double2*>(smem + g.lds_xchg);
                 uint64_t* const xr = reinterpret_cast<uint64_t*>(xm + LW);
-                int2* const xk = reinterpret_cast<int2*>(xr + 4 * LW);
+                int2* const xk = reinterpret_cast<int2*>(xr + 2 * Row::NW * LW);
+                constexpr int RW = 2 * Row::NW;  // u64 words of a pointer row
                 xm[lane] = make_double2(m0, m1);
-                xr[4 * lane] = row.a0; xr[4 * lane + 1] = row.a1;
-                xr[4 * lane + 2] = row.b0; xr[4 * lane + 3] = row.b1;
+#pragma unroll
+                for (int k = 0; k < Row::NW; ++k) {
+                    xr[RW * lane + k] = row.a[k];
+                    xr[RW * lane + Row::NW + k] = row.b[k];
+                }
                 __syncthreads();
                 int r0 = 0, r1 = 0;
                 for (int q = 0; q < nact; ++q) {
@@ -303,8 +330,11 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                 if (slot < nsurv) {
                     const double2 pv = xm[par];
                     pm = bit ? pv.y : pv.x;
-                    row.a0 = xr[4 * par]; row.a1 = xr[4 * par + 1];
-                    row.b0 = xr[4 * par + 2]; row.b1 = xr[4 * par + 3];
+#pragma unroll
+                    for (int k = 0; k < Row::NW; ++k) {
+                        row.a[k] = xr[RW * par + k];
+                        row.b[k] = xr[RW * par + Row::NW + k];
+                    }
                 } else {
                     pm = -INFINITY;
                 }
@@ -352,8 +382,11 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                 const int sl = c.base + par;
                 const double pa = bperm_d(sl, m0), pb = bperm_d(sl, m1);
                 Row nr;
-                nr.a0 = bperm64(sl, row.a0); nr.a1 = bperm64(sl, row.a1);
-                nr.b0 = bperm64(sl, row.b0); nr.b1 = bperm64(sl, row.b1);
+#pragma unroll
+                for (int k = 0; k < Row::NW; ++k) {
+                    nr.a[k] = bperm64(sl, row.a[k]);
+                    nr.b[k] = bperm64(sl, row.b[k]);
+                }
                 if (slot < nsurv) {
                     pm = bit ? pb : pa;
                     row = nr;
@@ -401,7 +434,7 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                     }
                     if (dd == 0) root_par = parity;
                 }
-                if (dd > 0) fill_pair(row.b0, row.b1, dd, dd + 1, slot);
+                if (dd > 0) fill_fields<Row>(row.b, dd, dd + 1, slot);
             }
             if constexpr (LCAP > 64) __syncthreads();  // other wavefronts' beta words
             else wave_fence();  // LDS is in order within a wave; only stop compiler reordering
@@ -508,7 +541,7 @@ static void* lane_pick_big(int F, int B) {
     return lane_pick_b<LCAP, false, 3>(B);
 }
 
-// defined in polar_lane_mid.hip (lists 16, 32) and polar_lane_big.hip (64..256)
+// defined in polar_lane_mid.hip (lists 16, 32) and polar_lane_big.hip (64..1024)
 void* lane_pick_mid(int lcap, int F, int B);
 void* lane_pick_large(int lcap, int F, int B);
 

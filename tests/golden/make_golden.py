@@ -246,6 +246,23 @@ def job_scl_l256():
 ROUND2_JOBS.append(job_scl_l256)
 
 
+def job_scl_l1024():
+    """Round 3: list sizes above 256 (16-bit path slots, one frame per workgroup
+    of up to 16 wavefronts): N=64 at L=512 and L=300 (a non-power-of-two list in
+    a 512-lane group), N=128 at L=1024, low SNR so the lists fill."""
+    out = {}
+    for tag, (N, K, L, snrs, frames, seed) in (("N64_L512", (64, 32, 512, (0.0, 1.0), 3, 321)),
+                                              ("N64_L300", (64, 40, 300, (0.5,), 3, 322)),
+                                              ("N128_L1024", (128, 64, 1024, (0.5,), 2, 323))):
+        d = job_scl(N, K, L, snrs, frames, seed, "x")[1]
+        for k in ("frozen", "llr", "msg", "snr", "scl", "ref_s_per_frame"):
+            out[tag + "_" + k] = d[k]
+    return "polar_scl_l1024.npz", out
+
+
+ROUND2_JOBS.append(job_scl_l1024)
+
+
 def job_small():
     """Small N, odd list sizes, K extremes, zero LLRs (deterministic cases)."""
     polar, _, channel = _imp()

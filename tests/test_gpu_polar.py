@@ -694,9 +694,10 @@ def test_scl_default_frozen_set_vs_oracle(gpu, oracle):
 
 
 def test_scl_large_lists_golden_and_oracle(gpu, oracle):
-    """List sizes 33..256 (lane kernel: one frame per wavefront up to 64, one
-    frame per workgroup of L/64 wavefronts above): the reference's L=64/128/256
-    fixtures, plus non-power-of-two sizes against the oracle."""
+    """List sizes 33..1024 (lane kernel: one frame per wavefront up to 64, one
+    frame per workgroup of L/64 wavefronts above, 16-bit path slots above 256):
+    the reference's L=64/128/256/300/512/1024 fixtures, plus non-power-of-two
+    sizes against the oracle; 1025 is refused."""
     P = _P()
     d = golden("polar_scl_l64.npz")
     for tag, N in (("N256", 256), ("N1024", 1024)):
@@ -721,8 +722,19 @@ def test_scl_large_lists_golden_and_oracle(gpu, oracle):
     llr64 = 2.0 * ((1.0 - 2.0 * cw) + 1.2 * rng.randn(24, 64)) / 1.44
     want = oracle.scl_decode(64, 256, fr64, llr64, threads=8)  # list outgrows 2^K paths: never pruned early
     assert _mismatch(P.SCLDecoder(64, 32, list_size=256, frozen_bits=fr64).decode_batch(llr64), want) == 0
-    with pytest.raises(ValueError):  # PL_EUNSUPPORTED: 8-bit path slots
-        P.SCLDecoder(N, K, list_size=257, frozen_bits=fr).decode_batch(llr)
+    # lists above 256: 16-bit path slots, one frame per workgroup of up to 16
+    # wavefronts (reference fixture + oracle, incl. a non-power-of-two list)
+    d = golden("polar_scl_l1024.npz")
+    for tag, Nt, L in (("N64_L512", 64, 512), ("N64_L300", 64, 300), ("N128_L1024", 128, 1024)):
+        fr_t = d[tag + "_frozen"]
+        dec = P.SCLDecoder(Nt, Nt - len(fr_t), list_size=L, frozen_bits=fr_t)
+        assert _mismatch(dec.decode_batch(d[tag + "_llr"]), d[tag + "_scl"]) == 0, tag
+    want = oracle.scl_decode(64, 700, fr64, llr64[:6], threads=8)
+    assert _mismatch(P.SCLDecoder(64, 32, list_size=700, frozen_bits=fr64).decode_batch(llr64[:6]), want) == 0
+    want = oracle.scl_decode(N, 513, fr, llr[:4], threads=8)
+    assert _mismatch(P.SCLDecoder(N, K, list_size=513, frozen_bits=fr).decode_batch(llr[:4]), want) == 0
+    with pytest.raises(ValueError):  # PL_EUNSUPPORTED: one workgroup (1024 lanes) per frame
+        P.SCLDecoder(N, K, list_size=1025, frozen_bits=fr).decode_batch(llr)
 
 
 @pytest.mark.parametrize("N,L,K", [(1024, 0, 300), (1024, 8, 512), (1024, 8, 40), (1024, 32, 700), (4096, 8, 2048),

@@ -153,6 +153,14 @@ def test_scl_l128_l256(oracle):
         assert _bad(oracle.scl_decode(N, L, d[tag + "_frozen"], d[tag + "_llr"], threads=8), d[tag + "_scl"]) == 0
 
 
+def test_scl_l512_l1024(oracle):
+    """List sizes above 256: 512, 300 (non-power-of-two) and 1024 (reference
+    SCLDecoder, round-3 fixture)."""
+    d = golden("polar_scl_l1024.npz")
+    for tag, N, L in (("N64_L512", 64, 512), ("N64_L300", 64, 300), ("N128_L1024", 128, 1024)):
+        assert _bad(oracle.scl_decode(N, L, d[tag + "_frozen"], d[tag + "_llr"], threads=8), d[tag + "_scl"]) == 0, tag
+
+
 def test_numpy_restatement_pinned():
     """oracle/refnumpy.py (the CPU baseline bench.py times as "the reference's
     NumPy path") reproduces the reference's outputs: SC / SCL on the config-1

@@ -333,12 +333,14 @@ PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int plane, int p
     constexpr int U = SQ < 8 ? SQ : 8;  // parent pairs in flight
 #pragma unroll 1
     for (int t0 = 0; t0 < SQ; t0 += U) {
-        double2 pr[U];
-#pragma unroll
-        for (int k = 0; k < U; ++k) pr[k] = src[(t0 + k) * 64];
+        // the partial-sum word first: waiting for it then leaves the pair
+        // loads in flight (each pair is waited for at its own fold)
         if constexpr (Q <= G::NB) {
             if ((t0 & 31) == 0) w = bsrc[(t0 >> 5) * 64];
         }
+        double2 pr[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) pr[k] = src[(t0 + k) * 64];
 #pragma unroll
         for (int k = 0; k < U; ++k)
             fold<G, Q>(st, g_op(pr[k].x, pr[k].y, w >> ((t0 + k) & 31)), t0 + k, smem, ws, plane);
@@ -380,11 +382,28 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
             lds_sync();  // the previous chunk's reads are issued before the overwrite
 #pragma unroll
             for (int h = 0; h < CH; ++h) stg[h * 64 + lane] = nxt[h];
-            if (c + 1 < NCH) {
+            // The chunk's partial-sum words (a chunk's elements lie in one word
+            // per depth), loaded BEFORE the next chunk's prefetch: the wait for
+            // a word then leaves the prefetch in flight.  (Loaded inside the
+            // element loop, after the prefetch, every word's join drained the
+            // prefetch with vmcnt(0) and each chunk paid a full memory latency.)
 #pragma unroll
-                for (int h = 0; h < CH; ++h) nxt[h] = src[((c + 1) * CH + h) * cstr];
+            for (int d = D0 + 1; d <= F; ++d) {
+                static_assert(32 % (IPC << (F - D0 - 1)) == 0, "a chunk's elements share one partial-sum word per depth");
+                const int e0 = (c * IPC) << (F - d);
+                if (d <= G::NB && right[d] && (e0 & 31) == 0) bw[d] = bsrc[d][(e0 >> 5) * 64];
+            }
+            {
+                // unconditional (the last chunk re-reads itself): a conditional
+                // prefetch made the compiler's wait for the words above a
+                // vmcnt(0) on the path without it, draining the prefetch
+                const int cn = c + 1 < NCH ? c + 1 : c;
+#pragma unroll
+                for (int h = 0; h < CH; ++h) nxt[h] = src[(cn * CH + h) * cstr];
             }
             lds_sync();
+            // (unrolled 2: the D0 = 0 chunks (IPC = 2) run without an inner
+            // loop, whose preheader would drain the prefetch with vmcnt(0))
 #pragma unroll 2
             for (int u = 0; u < IPC; ++u) {
                 const int t = c * IPC + u;
@@ -400,7 +419,6 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
                     const int e0 = t << (F - d);
                     const int m = 1 << (F - d);
                     if (right[d]) {
-                        if (d <= G::NB && (e0 & 31) == 0) bw[d] = bsrc[d][(e0 >> 5) * 64];
                         const uint32_t b = bw[d] >> (e0 & 31);
 #pragma unroll
                         for (int k = 0; k < m; ++k) v[k] = g_op(v[2 * k], v[2 * k + 1], b >> k);

@@ -402,9 +402,10 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
                 for (int h = 0; h < CH; ++h) nxt[h] = src[(cn * CH + h) * cstr];
             }
             lds_sync();
-            // (unrolled 2: the D0 = 0 chunks (IPC = 2) run without an inner
-            // loop, whose preheader would drain the prefetch with vmcnt(0))
-#pragma unroll 2
+            // (unrolled 2, 4 at LCAP = 16: the D0 = 0 chunks (IPC = 2, 4) run
+            // without an inner loop, whose preheader would drain the prefetch
+            // with vmcnt(0); full unrolling spills at LCAP = 8 / 32)
+#pragma unroll (G::LCAP == 16 ? 4 : 2)
             for (int u = 0; u < IPC; ++u) {
                 const int t = c * IPC + u;
                 double v[W];
@@ -993,13 +994,30 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                         const uint32_t* lsrc = reinterpret_cast<const uint32_t*>(ws + G::bl_off(dd <= G::NB ? dd : 1)) + ls;
                         uint32_t* ldst = reinterpret_cast<uint32_t*>(ws + G::bl_off(dd - 1 >= 1 ? dd - 1 : 1)) +
                                          G::pl(wslot, fw);
-                        for (int w = 0; w < 2 * cwc; ++w) {
-                            const uint32_t cwv = walkw[(parity * G::CW + (w >> 1)) * 64];
-                            const uint32_t lw = (dd > G::NB) ? bw5 : lsrc[(w >> 1) * 64];
-                            const int sh = (w & 1) * 16;
-                            const uint32_t r = spread16((lw ^ cwv) >> sh) | (spread16(cwv >> sh) << 1);
-                            if (last && dd - 1 > 0) ldst[w * 64] = r;
-                            else walkw[((parity ^ 1) * G::CW + w) * 64] = r;
+                        // word j of the step's input gives output words 2j, 2j+1
+                        // (one round trip per input word instead of per output
+                        // word; batching WB = 2 / 4 input words measured 7 / 16 %
+                        // slower at L = 8: spills)
+                        constexpr int WB = 1;
+                        uint32_t* const wdst = (last && dd - 1 > 0) ? ldst : walkw + (parity ^ 1) * G::CW * 64;
+#pragma unroll 1
+                        for (int j0 = 0; j0 < cwc; j0 += WB) {
+                            uint32_t cv[WB], lv[WB];
+#pragma unroll
+                            for (int u = 0; u < WB; ++u) {
+                                if (j0 + u < cwc) {  // wave-uniform
+                                    cv[u] = walkw[(parity * G::CW + j0 + u) * 64];
+                                    lv[u] = (dd > G::NB) ? bw5 : lsrc[(j0 + u) * 64];
+                                }
+                            }
+#pragma unroll
+                            for (int u = 0; u < WB; ++u) {
+                                if (j0 + u < cwc) {
+                                    const uint32_t x = lv[u] ^ cv[u];
+                                    wdst[(2 * (j0 + u)) * 64] = spread16(x) | (spread16(cv[u]) << 1);
+                                    wdst[(2 * (j0 + u) + 1) * 64] = spread16(x >> 16) | (spread16(cv[u] >> 16) << 1);
+                                }
+                            }
                         }
                         parity ^= 1;
                         --dd;

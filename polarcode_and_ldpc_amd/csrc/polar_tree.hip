@@ -393,20 +393,31 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
                 const int e0 = (c * IPC) << (F - d);
                 if (d <= G::NB && right[d] && (e0 & 31) == 0) bw[d] = bsrc[d][(e0 >> 5) * 64];
             }
-            {
-                // unconditional (the last chunk re-reads itself): a conditional
-                // prefetch made the compiler's wait for the words above a
-                // vmcnt(0) on the path without it, draining the prefetch
+            // the next chunk's prefetch: unconditional (the last chunk re-reads
+            // itself; a conditional one made the compiler's wait for the words
+            // above a vmcnt(0) on the path without it, draining the prefetch)
+            constexpr int UNR = G::LCAP == 16 ? 4 : 2;  // element-loop unroll
+            auto prefetch = [&]() {
                 const int cn = c + 1 < NCH ? c + 1 : c;
 #pragma unroll
                 for (int h = 0; h < CH; ++h) nxt[h] = src[(cn * CH + h) * cstr];
-            }
+            };
+            // no inner loop (IPC <= UNR): issued here.  Otherwise (LCAP >= 16)
+            // inside the loop's first iteration: the loop preheader waits
+            // vmcnt(0) for the words above and would drain a prefetch issued
+            // before it (L = 16 -2.3 %, L = 32 -1 %; at LCAP = 8, whose inner
+            // loops are the short D0 = 1, 2 passes, +3 %: spills).
+            constexpr bool PF_IN = IPC > UNR && G::LCAP >= 16;
+            if constexpr (!PF_IN) prefetch();
             lds_sync();
             // (unrolled 2, 4 at LCAP = 16: the D0 = 0 chunks (IPC = 2, 4) run
             // without an inner loop, whose preheader would drain the prefetch
             // with vmcnt(0); full unrolling spills at LCAP = 8 / 32)
-#pragma unroll (G::LCAP == 16 ? 4 : 2)
+#pragma unroll UNR
             for (int u = 0; u < IPC; ++u) {
+                if constexpr (PF_IN) {
+                    if (u == 0) prefetch();
+                }
                 const int t = c * IPC + u;
                 double v[W];
 #pragma unroll

@@ -65,6 +65,20 @@ namespace {
 #ifndef PL_ORDERED_PRUNE
 #define PL_ORDERED_PRUNE 16  // list capacities >= this skip ranking when the full list stays ordered (ordered_prune)
 #endif
+// SC instances hold 31 KB of LDS per wave (5 waves per CU, ~1 per SIMD), so
+// nothing hides a wave's latencies but its own loads in flight: a 256-VGPR
+// budget, 16 workspace pairs per g batch and the channel loop unrolled 8
+// (measured together: N=1024 -4 %, default set -2.6 %, N=256 -3.8 %, N=4096
+// -10.6 %, bits identical; profiles/r03_e/ab_sc_knobs.log)
+#ifndef PL_SC_WPE
+#define PL_SC_WPE 2  // SC instances: waves per SIMD their register budget is built for
+#endif
+#ifndef PL_SC_U
+#define PL_SC_U 16  // SC instances: workspace parent pairs in flight per g-chain batch
+#endif
+#ifndef PL_SC_FUNROLL
+#define PL_SC_FUNROLL 8  // SC instances: unroll of the depth-1 loop over the channel
+#endif
 #ifndef PL_RANK_F32
 #define PL_RANK_F32 1  // strict ranks from fp32 roundings of the metrics (collisions fall back)
 #endif
@@ -330,7 +344,8 @@ PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int plane, int p
     uint32_t w = 0;
     if constexpr (Q > G::NB) w = beta_get<n>(Q, bb, bw5);
     const uint32_t* bsrc = reinterpret_cast<const uint32_t*>(ws + G::bl_off(Q <= G::NB ? Q : 1)) + bs;
-    constexpr int U = SQ < 8 ? SQ : 8;  // parent pairs in flight
+    constexpr int UM = G::LCAP == 1 ? PL_SC_U : 8;
+    constexpr int U = SQ < UM ? SQ : UM;  // parent pairs in flight
 #pragma unroll 1
     for (int t0 = 0; t0 < SQ; t0 += U) {
         // the partial-sum word first: waiting for it then leaves the pair
@@ -445,7 +460,7 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
         return st.lam;
     }
     const double2* src = reinterpret_cast<const double2*>(ws + G::st_off(D0)) + fw;
-#pragma unroll 2
+#pragma unroll (G::LCAP == 1 ? PL_SC_FUNROLL : 2)
     for (int t = 0; t < SF; ++t) {
         double v[W];
         if constexpr (G::STAGE) {
@@ -1160,12 +1175,12 @@ const TreeEntry* tree_table(int* count) {
         // lane) and five LDS depths (62 doubles per frame, 31 KB per wave, 5
         // waves per CU): N=1024 1.88 -> 1.28 ms, N=4096 5.78 -> 4.47 ms against
         // F = 3, DL = n-3 (profiles/r03_d/ab_sc_tiers.log)
-        make_entry<7, 1, true, 1, 2>(),
-        make_entry<8, 1, true, 1, 3>(),
-        make_entry<9, 1, true, 1, 4>(),
-        make_entry<10, 1, true, 1, 5>(),
-        make_entry<11, 1, true, 1, 6>(),
-        make_entry<12, 1, true, 1, 7>(),
+        make_entry<7, 1, true, 1, 2, false, PL_SC_WPE>(),
+        make_entry<8, 1, true, 1, 3, false, PL_SC_WPE>(),
+        make_entry<9, 1, true, 1, 4, false, PL_SC_WPE>(),
+        make_entry<10, 1, true, 1, 5, false, PL_SC_WPE>(),
+        make_entry<11, 1, true, 1, 6, false, PL_SC_WPE>(),
+        make_entry<12, 1, true, 1, 7, false, PL_SC_WPE>(),
 #if PL_DIAG  // after the product entries: picked only through PL_TREE_F / PL_TREE_DL(OFF)
         make_entry<10, 32, false, 4, 7>(),
         make_entry<10, 32, false, 2, 7>(),

@@ -67,17 +67,17 @@ namespace {
 #endif
 // SC instances hold 31 KB of LDS per wave (5 waves per CU, ~1 per SIMD), so
 // nothing hides a wave's latencies but its own loads in flight: a 256-VGPR
-// budget, 16 workspace pairs per g batch and the channel loop unrolled 8
-// (measured together: N=1024 -4 %, default set -2.6 %, N=256 -3.8 %, N=4096
-// -10.6 %, bits identical; profiles/r03_e/ab_sc_knobs.log)
+// budget, 32 workspace pairs per g batch and the channel loop unrolled 16
+// (against 8 pairs / unroll 2: N=1024 -5 %, default set -4 %, N=256 -7 %,
+// N=4096 -12 %, bits identical; profiles/r03_e/ab_sc_knobs*.log)
 #ifndef PL_SC_WPE
 #define PL_SC_WPE 2  // SC instances: waves per SIMD their register budget is built for
 #endif
 #ifndef PL_SC_U
-#define PL_SC_U 16  // SC instances: workspace parent pairs in flight per g-chain batch
+#define PL_SC_U 32  // SC instances: workspace parent pairs in flight per g-chain batch
 #endif
 #ifndef PL_SC_FUNROLL
-#define PL_SC_FUNROLL 8  // SC instances: unroll of the depth-1 loop over the channel
+#define PL_SC_FUNROLL 16  // SC instances: unroll of the depth-1 loop over the channel
 #endif
 #ifndef PL_RANK_F32
 #define PL_RANK_F32 1  // strict ranks from fp32 roundings of the metrics (collisions fall back)

@@ -1186,8 +1186,8 @@ const TreeEntry* tree_table(int* count) {
         make_entry<10, 32, false, 2, 7>(),
         make_entry<10, 1, true, 3, 7>(),
         make_entry<10, 1, true, 2, 7>(),
-        make_entry<10, 1, true, 1, 6>(),
-        make_entry<10, 1, true, 1, 4>(),
+        make_entry<10, 1, true, 1, 6, false, PL_SC_WPE>(),
+        make_entry<10, 1, true, 1, 4, false, PL_SC_WPE>(),
 #endif
     };
     *count = (int)(sizeof(tab) / sizeof(tab[0]));

@@ -79,6 +79,9 @@ namespace {
 #ifndef PL_SC_FUNROLL
 #define PL_SC_FUNROLL 16  // SC instances: unroll of the depth-1 loop over the channel
 #endif
+#ifndef PL_DEDUP_NMAX
+#define PL_DEDUP_NMAX 10  // largest n whose fused top de-duplicates its staged reads
+#endif
 #ifndef PL_RANK_F32
 #define PL_RANK_F32 1  // strict ranks from fp32 roundings of the metrics (collisions fall back)
 #endif
@@ -264,7 +267,7 @@ struct TG {
     // chunk; n <= 10 only (at N = 2048 / 4096, L = 8 it measured slower, 8.7 /
     // 13.0 ms against 8.3 / 12.0)
     static constexpr bool dedup(int D0) {
-        return STAGE && n <= 10 && LCAP >= (1 << (F - D0)) / 2 && (1 << (n - F)) * ((1 << (F - D0)) / 2) >= LCAP;
+        return STAGE && n <= PL_DEDUP_NMAX && LCAP >= (1 << (F - D0)) / 2 && (1 << (n - F)) * ((1 << (F - D0)) / 2) >= LCAP;
     }
     static PL_DEV int pl(int s, int f) { return SHADOW ? s * FPW + f : f * LCAP + s; }
 };

@@ -342,7 +342,7 @@ def _bench_headline(args, rt, pool, N, K, L, B):
     if pool is not None:
         from oracle import oracle as O
         from oracle import refnumpy as R
-        S, S1, S2 = args.cpu_frames_numpy, 8, args.cpu_frames
+        S, S1, S2 = min(args.cpu_frames_numpy, B), min(8, B), min(args.cpu_frames, B)
         llr_h = llr[:max(S, S2)].cpu().numpy()
         got = out[:llr_h.shape[0]].cpu().numpy().astype(np.int64)
         procs = cpu_processes()
@@ -360,6 +360,7 @@ def _bench_headline(args, rt, pool, N, K, L, B):
         ec = torch.zeros(3, dtype=torch.int64, device="cuda")
         sc = torch.zeros(3, dtype=torch.int64, device="cuda")
         stepno = [0]
+        ekt = KernelTimer()
         msg2, out2 = torch.empty_like(msg), torch.empty_like(out)
         cw2 = torch.empty((B, N), dtype=torch.uint8, device="cuda")
         llr2 = torch.empty_like(llr)
@@ -370,16 +371,23 @@ def _bench_headline(args, rt, pool, N, K, L, B):
             _native.random_bits(43, o, msg2)
             _native.polar_encode(plan, msg2, cw2)
             ch.llr_batch_device(cw2, N, B, seed=43, frame_offset=o, out=llr2)
-            plan.decode(llr2, out2)
+            ekt(lambda: plan.decode(llr2, out2))
             sc.zero_()
             _native.count_errors(msg2, out2, K, sc)
             rt.all_reduce(sc)
             ec.add_(sc)
 
-        edt, _ = timed_steps(e2e_step, args.steps, args.warmup, rt, on_timed=ec.zero_)
+        def e2e_start():
+            ec.zero_()
+            ekt.reset()
+
+        edt, _ = timed_steps(e2e_step, args.steps, args.warmup, rt, on_timed=e2e_start)
         e = ec.cpu().numpy()
+        ekms = ekt.mean_ms()
         res["end_to_end"] = dict(value=B * rt.world * args.steps * K / edt / 1e6, unit="info-Mbps",
-                                 ms_per_step=edt / args.steps * 1e3,
+                                 ms_per_step=edt / args.steps * 1e3, kernel_ms=ekms,
+                                 roofline=roofline("polar_scl_1024_l8", polar_kernel_name(plan, 10), B, 8 * N + K,
+                                                   ekms),
                                  what="per step: device random messages + polar encode + AWGN LLRs (Philox) + "
                                       "SCL decode + error count (+ all-reduce)",
                                  ber=float(e[0]) / max(1, e[2] * K), fer=float(e[1]) / max(1, e[2]))
@@ -410,7 +418,7 @@ def bench_polar(args, rt, pool):
             roofline=roofline("polar_scl_1024_l8_default", polar_kernel_name(dd.plan, 10), B, 8 * N + K, dkms))
         if pool is not None:
             from oracle import refnumpy as R
-            S = args.cpu_frames_numpy
+            S = min(args.cpu_frames_numpy, B)
             lh = dllr[:S].cpu().numpy()
             res["default_frozen_set"]["cpu_baseline"] = numpy_baseline(
                 pool, cpu_processes(), "SCL N=1024 L=%d, default frozen set" % L,
@@ -475,7 +483,7 @@ def bench_sc_default(args, rt, pool):
     if pool is not None:
         from oracle import oracle as O
         from oracle import refnumpy as R
-        S, S1, S2 = 1024, 64, 16384
+        S, S1, S2 = min(1024, B), min(64, B), min(16384, B)
         lh = llr[:S2].cpu().numpy()
         got = out[:S2].cpu().numpy().astype(np.int64)
         fr = dec.frozen_bits
@@ -563,16 +571,20 @@ def bench_ldpc(args, rt, pool):
         # codeword-symmetric) at the same SNR, early stop on.
         llr0 = AWGNChannel(args.snr).llr_batch_device(None, n, B, seed=4243, frame_offset=rt.rank * B)
         out0, its0 = torch.empty_like(out), torch.empty_like(its)
-        dt0, pr0 = timed_steps(lambda: plan.decode(llr0, out0, its0), args.steps, args.warmup, rt)
+        vkt = KernelTimer()
+        dt0, pr0 = timed_steps(lambda: vkt(lambda: plan.decode(llr0, out0, its0)), args.steps, args.warmup, rt,
+                               on_timed=vkt.reset)
+        vkms = vkt.mean_ms()
         res["valid_codewords"] = dict(value=B * rt.world * args.steps * k / dt0 / 1e6, unit="info-Mbps",
-                                      ms_per_step=dt0 / args.steps * 1e3,
+                                      ms_per_step=dt0 / args.steps * 1e3, kernel_ms=vkms,
+                                      roofline=roofline("ldpc_bp_504_valid", kname, B, 9 * n, vkms),
                                       rank_ms_per_step=[t / args.steps * 1e3 for t in pr0],
                                       mean_iterations=float(its0.double().mean().item()),
                                       bit_errors=int(out0.sum().item()),
                                       what="all-zero codeword frames (device AWGN), BP max_iter=20, early stop")
         if pool is not None:
             from oracle import refnumpy as R
-            S = args.cpu_frames_numpy
+            S = min(args.cpu_frames_numpy, B)
             lh = llr0[:S].cpu().numpy()
             res["valid_codewords"]["cpu_baseline"] = numpy_baseline(
                 pool, cpu_processes(), "BP-20 (504,252), all-zero codewords, early stop",
@@ -583,7 +595,7 @@ def bench_ldpc(args, rt, pool):
         from oracle import oracle as O
         from oracle import refnumpy as R
         from polarcode_and_ldpc_amd.ldpc import dense_to_csr
-        S, S1, S2 = args.cpu_frames_numpy, 8, args.cpu_frames_ldpc
+        S, S1, S2 = min(args.cpu_frames_numpy, B), min(8, B), min(args.cpu_frames_ldpc, B)
         llr_h = llr[:max(S, S2)].cpu().numpy()
         got = out[:llr_h.shape[0]].cpu().numpy().astype(np.int64)
         procs = cpu_processes()
@@ -633,7 +645,7 @@ def bench_cascl(args, rt, pool=None):
         from oracle import oracle as O
         from oracle import refnumpy as R
         from polarcode_and_ldpc_amd.polar import SCLDecoder
-        S, S2 = args.cpu_frames_l32, 64
+        S, S2 = min(args.cpu_frames_l32, B), min(64, B)
         lh = llr[:max(S, S2)].cpu().numpy()
         procs = cpu_processes()
         plain = SCLDecoder(N, K, L, frozen_bits=fr).decode_batch(torch.from_numpy(lh[:S]).cuda())
@@ -685,7 +697,7 @@ def _long_polar(rt, B, steps, pool=None):
     if pool is not None:
         from oracle import oracle as O
         from oracle import refnumpy as R
-        S, S2 = 16, 128
+        S, S2 = min(16, B), min(128, B)
         lh = llr[:S2].cpu().numpy()
         got = out[:S2].cpu().numpy().astype(np.int64)
         procs = cpu_processes()
@@ -722,7 +734,7 @@ def _long_ms(rt, B, steps, es, pool=None):
         from oracle import oracle as O
         from oracle import refnumpy as R
         from polarcode_and_ldpc_amd.ldpc import dense_to_csr
-        S, S2 = 16, 512
+        S, S2 = min(16, B), min(512, B)
         lh = llr[:S2].cpu().numpy()
         got = out[:S2].cpu().numpy().astype(np.int64)
         procs = cpu_processes()
@@ -769,6 +781,127 @@ def bench_stub(args, rt):
                 counts=[int(x) for x in counts.tolist()], B=B)
 
 
+# ---------------------------------------------------------------- output
+MAX_LINE = 6000  # the driver keeps ~8 KB of stdout: the one JSON line must fit well inside it
+PMC_NOTE = ("roofline.traffic: HBM-side bytes per launch (2*FETCH_SIZE+WRITE_SIZE, gfx950 correction) from a "
+            "separate rocprofv3 --pmc pass of the same build at the same batch (profiles/pmc_traffic.json); "
+            "achieved/frac from algorithmic bytes over HIP-event kernel time in this run")
+
+
+def _r(x, sig=4):
+    """Round floats to `sig` significant digits (None / ints / strings pass)."""
+    if isinstance(x, float):
+        if x != x or x in (float("inf"), float("-inf")):
+            return None
+        return float("%.*g" % (sig, x))
+    if isinstance(x, dict):
+        return {k: _r(v, sig) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_r(v, sig) for v in x]
+    return x
+
+
+def _roof_short(r):
+    if not r:
+        return None
+    return _r(dict(bound=r.get("bound"), achieved=r.get("achieved"), peak=r.get("peak"), unit=r.get("unit"),
+                   frac=r.get("frac"), traffic=r.get("traffic"), kernel=r.get("kernel"),
+                   kernel_ms=r.get("kernel_ms"), frames=r.get("frames_per_launch")))
+
+
+def _cpu_short(c, with_sample=False):
+    if not c:
+        return None
+    out = dict(value=c.get("value"), unit=c.get("unit"), cores=c.get("cores"), kind=c.get("kind"),
+               mismatches=c.get("mismatching_frames_vs_gpu"))
+    if with_sample:
+        out["sample"] = c.get("sample")
+    if c.get("single_core"):
+        out["single_core"] = c["single_core"].get("value")
+    if c.get("c_port"):
+        out["c_port"] = c["c_port"].get("value")
+        out["c_port_mismatches"] = c["c_port"].get("mismatching_frames_vs_gpu")
+    return _r(out)
+
+
+def _key_short(k):
+    """value, ms_per_step, kernel_ms, roofline frac / traffic, CPU figures of one secondary key."""
+    r = k.get("roofline") or {}
+    c = k.get("cpu_baseline") or {}
+    out = dict(value=k.get("value"), ms_per_step=k.get("ms_per_step"), kernel_ms=k.get("kernel_ms"),
+               frac=r.get("frac"), traffic=r.get("traffic"))
+    for f in ("mean_iterations", "fer"):
+        if k.get(f) is not None:
+            out[f] = k[f]
+    if c:
+        out["cpu"] = c.get("value")
+        out["cpu_cores"] = c.get("cores")
+        out["cpu_mismatches"] = c.get("mismatching_frames_vs_gpu")
+        if c.get("c_port"):
+            out["cpu_c_port"] = c["c_port"].get("value")
+    return _r(out)
+
+
+def compact_line(full, detail_path=None):
+    """The one stdout line: the contract fields, the headline roofline and
+    cpu_baseline, and a compact summary of every secondary key.  Wave shares,
+    VALU splits, per-rank detail of the secondary keys and the sweep's
+    intervals go to the detail file (`--detail-out`)."""
+    line = {k: full.get(k) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                     "rank_ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype",
+                                     "data", "config")}
+    line = _r(line, 6)
+    line["roofline"] = _roof_short(full.get("roofline"))
+    if line["roofline"] is not None:
+        line["roofline"]["traffic_source"] = "separate PMC pass (see pmc_note)"
+    line["cpu_baseline"] = _cpu_short(full.get("cpu_baseline"), with_sample=True)
+    line["ber"], line["fer"] = _r(full.get("ber")), _r(full.get("fer"))
+    keys = {}
+    for name in ("end_to_end", "default_frozen_set", "polar_sc_default", "config0_sc_256", "ldpc", "cascl_l32"):
+        if full.get(name):
+            keys[name] = _key_short(full[name])
+    if full.get("ldpc", {}).get("valid_codewords"):
+        keys["ldpc.valid_codewords"] = _key_short(full["ldpc"]["valid_codewords"])
+    sw = (full.get("cascl_l32") or {}).get("sweep")
+    if sw:
+        keys["cascl_l32.sweep"] = dict(seconds=_r(sw.get("seconds")),
+                                       points=[[p["snr_db"], p["frames"], p["frame_errors"], _r(p["ber"], 3),
+                                                _r(p["fer"], 3)] for p in sw.get("points", [])],
+                                       cols="snr_db,frames,frame_errors,ber,fer")
+    for name, v in (full.get("long_block") or {}).items():
+        keys["long_block." + name] = _key_short(v)
+    line["keys"] = keys
+    line["pmc_note"] = PMC_NOTE
+    if detail_path:
+        line["detail"] = detail_path
+    s = json.dumps(line)
+    if len(s) > MAX_LINE:  # never exceed the driver's tail: drop the secondary keys' CPU figures, then samples
+        for v in keys.values():
+            for f in ("cpu_cores", "cpu_mismatches", "cpu_c_port", "ms_per_step"):
+                v.pop(f, None)
+        if line["cpu_baseline"]:
+            line["cpu_baseline"].pop("sample", None)
+        line["pmc_note"] = "traffic from a separate PMC pass (profiles/pmc_traffic.json)"
+    return line
+
+
+def write_detail(full, path):
+    """The full result (wave shares, VALU splits, per-rank times, samples, sweep
+    intervals) as JSON; returns the path written (relative to the repo) or None."""
+    if not path:
+        return None
+    p = path if os.path.isabs(path) else os.path.join(ROOT, path)
+    try:
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "w") as f:
+            json.dump(full, f, indent=1)
+    except OSError as e:
+        log("bench.py: could not write the detail file %s: %s" % (p, e))
+        return None
+    log("bench.py: full result in %s" % p)
+    return os.path.relpath(p, ROOT)
+
+
 # ---------------------------------------------------------------- main
 def self_launch(args):
     """--gpus N > 1 without a torch.distributed environment: start N ranks under
@@ -810,6 +943,8 @@ def main():
                     help="only the headline decodes (no end-to-end / valid-codeword / configs[3,4] runs)")
     ap.add_argument("--sections", default=None,
                     help="comma list of " + ",".join(SECTIONS) + " (profiling passes: one kernel per section)")
+    ap.add_argument("--detail-out", default="gpurun_out/bench_detail.json",
+                    help="file for the full result (stdout carries one compact line); '' = none")
     ap.add_argument("--cpu-stub", action="store_true", help="CPU/gloo plumbing check with a stub decode")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: host-side counter reduction, ranks may share one GPU (rehearsal only)")
@@ -865,7 +1000,7 @@ def main():
     if pool is not None:
         pool.close()
     if rt.rank == 0:
-        line = {
+        full = {
             "metric": METRIC, "value": pol.get("value"), "unit": "info-Mbps", "n_gpus": rt.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": pol.get("ms_per_step"),
             "rank_ms_per_step": pol.get("rank_ms_per_step"),
@@ -882,9 +1017,10 @@ def main():
             "default_frozen_set": pol.get("default_frozen_set"),
         }
         if ldp is not None:
-            line["ldpc"] = ldp
-        line.update(extra)
-        print(json.dumps(line), flush=True)
+            full["ldpc"] = ldp
+        full.update(extra)
+        path = write_detail(full, args.detail_out)
+        print(json.dumps(compact_line(full, path)), flush=True)
     rt.close()
 
 

@@ -117,7 +117,9 @@ int pl_decode_ws(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld
 /* Pre-allocate `stream`'s workspace for batches up to max_batch, so that
  * pl_decode on that stream never allocates (max_batch == 0: pl_plan_release).
  * If the device cannot hold the full-speed size, the largest halving of at
- * least one unit is kept (fewer resident wavefronts, same results). */
+ * least one unit is kept (fewer resident wavefronts, same results) and later
+ * decodes of up to max_batch frames run on it without retrying the allocation;
+ * only another pl_plan_reserve (or a larger batch) retries. */
 int pl_plan_reserve(pl_plan* plan, int64_t max_batch, void* stream);
 
 /* Free `stream`'s workspace (after draining that stream).  A finished stream's
@@ -132,8 +134,12 @@ int pl_plan_get_info(const pl_plan* plan, pl_plan_info* info);
 int pl_plan_destroy(pl_plan* plan);
 const char* pl_last_error(void);
 
-/* Every call taking a plan must run with the plan's device current (the device
- * current at plan creation); otherwise it returns PL_EINVAL and does nothing. */
+/* Calls that touch a plan's device memory -- pl_decode, pl_decode_ws,
+ * pl_plan_reserve, pl_plan_release, pl_polar_plan_set_crc, pl_polar_encode,
+ * pl_debug_polar_stamps -- must run with the plan's device current (the device
+ * current at plan creation); otherwise they return PL_EINVAL and do nothing.
+ * pl_plan_get_info, pl_plan_workspace_bytes and pl_plan_workspace_stats read
+ * host state only; pl_plan_destroy may run on any device. */
 
 /* Diagnostic build only (make DIAG=1; the product library returns
  * PL_EUNSUPPORTED): pl_decode of a polar plan through an instrumented kernel that adds
@@ -145,8 +151,10 @@ const char* pl_last_error(void);
 int pl_debug_polar_stamps(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
                           unsigned long long* stamps_dev, void* stream);
 
-/* Test hook: overwrite the device id a plan is bound to, so the wrong-device
- * check can be exercised on a one-GPU machine.  Not for production use. */
+/* Test hook, diagnostic build only (the product library returns
+ * PL_EUNSUPPORTED): overwrite the device id a plan is bound to, so the
+ * wrong-device check can be exercised on a one-GPU machine.  UNSAFE: it turns
+ * the wrong-device protection off for that plan. */
 int pl_debug_set_plan_device(pl_plan* plan, int32_t device);
 
 /* ---- Monte-Carlo frame source (replaces src/channel/awgn.py:91-112 and the

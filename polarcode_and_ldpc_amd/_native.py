@@ -34,13 +34,13 @@ class PlanInfo(ctypes.Structure):
                 ("frames_per_block", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
+def _load(path=LIB_PATH):
+    if not os.path.exists(path):
         raise ImportError(
             "polarcode_and_ldpc_amd: native library %s not found -- build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` (make -C polarcode_and_ldpc_amd/csrc). "
-            "There is no CPU fallback." % LIB_PATH)
-    L = ctypes.CDLL(LIB_PATH)
+            "There is no CPU fallback." % path)
+    L = ctypes.CDLL(path)
     P, I32, I64, D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
     PP = ctypes.POINTER(ctypes.c_void_p)
     L.pl_polar_plan_create.argtypes = [I32, I32, P, I32, I32, PP]
@@ -72,6 +72,13 @@ def _load():
 
 lib = _load()
 _BUILD_ID = None
+DIAG_LIB_PATH = os.path.join(_HERE, "_lib", "diag", "libpolarldpc_diag.so")
+
+
+def load_diag():
+    """The diagnostic build (make diag: stamped kernels, test hooks), bound like
+    the product library, or None if it was not built.  Tests and tools only."""
+    return _load(DIAG_LIB_PATH) if os.path.exists(DIAG_LIB_PATH) else None
 
 
 def build_id() -> str:

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -23,7 +24,13 @@
 struct Workspace {
     std::mutex mu;
     void* ptr = nullptr;
-    size_t bytes = 0;
+    // written under `mu`; atomic so pl_plan_workspace_stats may read it under the map mutex only
+    std::atomic<size_t> bytes{0};
+    // after an out-of-memory fallback: the request that did not fit.  Later decodes
+    // needing no more than it run on the smaller buffer (decode_impl clamps the grid)
+    // instead of draining and retrying the allocation every call; pl_plan_reserve,
+    // or a larger request, retries.
+    size_t failed_need = 0;
     ~Workspace() {
         if (ptr) hipFree(ptr);  // hipFree waits for work that still uses it
     }
@@ -405,30 +412,48 @@ static std::shared_ptr<Workspace> stream_entry(pl_plan* p, hipStream_t s) {
 }
 
 // Grow `w` (its mutex held by the caller) to `need` bytes.  A buffer is only
-// ever used by its own stream, so before it is replaced only that stream has to
-// drain.  If the device cannot hold `need`, fall back to the largest halving
-// that is still at least one unit (the decode then runs fewer resident
-// wavefronts / smaller chunks, decode_impl clamps to what the buffer holds).
-static int grow_ws(pl_plan* p, Workspace* w, hipStream_t s, size_t need) {
+// ever used by its own stream.  The new buffer is allocated while the old one
+// is still held; only if the device is out of memory is the old one released
+// (after draining its stream) before retrying, then halved down to one unit (the
+// decode then runs fewer resident wavefronts / smaller chunks: decode_impl
+// clamps to what the buffer holds).  A failure other than out-of-memory leaves
+// the old buffer in place.  `retry`: also retry a request that fell back before.
+static int grow_ws(pl_plan* p, Workspace* w, hipStream_t s, size_t need, bool retry) {
     if (w->bytes >= need) return PL_OK;
-    if (w->ptr) {
-        hipError_t e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return hipfail(e, "workspace regrow: stream synchronize");
-        hipFree(w->ptr);
-        w->ptr = nullptr;
-        w->bytes = 0;
-    }
+    if (!retry && w->ptr && w->failed_need && need <= w->failed_need) return PL_OK;  // fell back for this size
     const size_t unit = std::max<size_t>(p->ws_unit, 1);
     size_t want = need;
     for (;;) {
-        hipError_t e = hipMalloc(&w->ptr, want);
+        void* np = nullptr;
+        hipError_t e = hipMalloc(&np, want);
         if (e == hipSuccess) {
+            if (w->ptr) {
+                // the old buffer may still be read by work queued on this stream
+                hipError_t se = hipStreamSynchronize(s);
+                hipFree(w->ptr);
+                w->ptr = nullptr;
+                w->bytes = 0;
+                if (se != hipSuccess) {
+                    hipFree(np);
+                    return hipfail(se, "workspace regrow: stream synchronize");
+                }
+            }
+            w->ptr = np;
             w->bytes = want;
+            w->failed_need = want < need ? need : 0;
             return PL_OK;
         }
-        w->ptr = nullptr;
         (void)hipGetLastError();  // clear the sticky allocation error before retrying
-        if (e != hipErrorOutOfMemory || want <= unit) return hipfail(e, "decode workspace");
+        if (e != hipErrorOutOfMemory) return hipfail(e, "decode workspace");
+        if (w->ptr) {  // make room: drain this stream, release its buffer, retry the same size
+            hipError_t se = hipStreamSynchronize(s);
+            hipFree(w->ptr);
+            w->ptr = nullptr;
+            w->bytes = 0;
+            if (se != hipSuccess) return hipfail(se, "workspace regrow: stream synchronize");
+            continue;
+        }
+        if (want <= unit) return hipfail(e, "decode workspace");
         want = std::max(unit, (want / 2) / unit * unit);
     }
 }
@@ -453,11 +478,12 @@ extern "C" int pl_plan_reserve(pl_plan* p, int64_t max_batch, void* stream) {
     const hipStream_t s = (hipStream_t)stream;
     std::shared_ptr<Workspace> w = stream_entry(p, s);
     std::lock_guard<std::mutex> lk(w->mu);
-    return grow_ws(p, w.get(), s, need);
+    return grow_ws(p, w.get(), s, need, true);
 }
 
 extern "C" int pl_plan_release(pl_plan* p, void* stream) {
     if (!p) return fail(PL_EINVAL, "plan is NULL");
+    if (int rc = check_device(p)) return rc;
     const hipStream_t s = (hipStream_t)stream;
     std::shared_ptr<Workspace> w;
     {
@@ -485,7 +511,7 @@ extern "C" int pl_plan_workspace_stats(const pl_plan* p, int64_t* streams, int64
     *bytes = 0;
     for (const auto& kv : p->ws) {
         ++*streams;
-        *bytes += (int64_t)kv.second->bytes;  // racy read of a size_t, diagnostic only
+        *bytes += (int64_t)kv.second->bytes.load();
     }
     return PL_OK;
 }
@@ -507,7 +533,7 @@ extern "C" int pl_decode(pl_plan* p, const double* llr, int64_t batch, int64_t l
     if (!need) return decode_impl(p, llr, batch, ld, bits, iters, nullptr, 0, nullptr, s);
     std::shared_ptr<Workspace> w = stream_entry(p, s);
     std::lock_guard<std::mutex> lk(w->mu);
-    if ((rc = grow_ws(p, w.get(), s, need))) return rc;
+    if ((rc = grow_ws(p, w.get(), s, need, false))) return rc;
     return decode_impl(p, llr, batch, ld, bits, iters, w->ptr, w->bytes, nullptr, s);
 }
 
@@ -534,15 +560,20 @@ extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batc
     const hipStream_t s = (hipStream_t)stream;
     std::shared_ptr<Workspace> w = stream_entry(p, s);
     std::lock_guard<std::mutex> lk(w->mu);
-    if ((rc = grow_ws(p, w.get(), s, ws_need(p, batch)))) return rc;
+    if ((rc = grow_ws(p, w.get(), s, ws_need(p, batch), false))) return rc;
     return decode_impl(p, llr, batch, ld, bits, nullptr, w->ptr, w->bytes, stamps_dev, s);
 #endif
 }
 
 extern "C" int pl_debug_set_plan_device(pl_plan* p, int32_t device) {
     if (!p) return fail(PL_EINVAL, "plan is NULL");
+#if !PL_DIAG
+    (void)device;
+    return fail(PL_EUNSUPPORTED, "test hook: diagnostic build only (make DIAG=1)");
+#else
     p->device = device;
     return PL_OK;
+#endif
 }
 
 extern "C" int pl_polar_plan_set_crc(pl_plan* p, int32_t crc_len, uint32_t poly) {

@@ -463,7 +463,8 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
         return st.lam;
     }
     const double2* src = reinterpret_cast<const double2*>(ws + G::st_off(D0)) + fw;
-#pragma unroll (G::LCAP == 1 ? PL_SC_FUNROLL : 2)
+    constexpr int kChUnroll = G::LCAP == 1 ? PL_SC_FUNROLL : 2;
+#pragma unroll kChUnroll
     for (int t = 0; t < SF; ++t) {
         double v[W];
         if constexpr (G::STAGE) {

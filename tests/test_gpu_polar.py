@@ -1,6 +1,8 @@
 """Parity of the HIP polar decoders (through the C-ABI via the drop-in classes)
 against (a) the reference's own outputs (golden fixtures, tests/golden/) and
 (b) the C oracle on fresh seeded inputs.  Bar: bit-exact decoded bits."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -624,20 +626,40 @@ def test_release_and_wrong_device(gpu):
     plan.reserve(0)  # reserve(0) = release
     assert plan.workspace_stats() == (0, 0)
 
+    # the wrong-device refusal, through the diagnostic build's test hook (the
+    # product library does not carry it: ADVICE r03)
+    assert _native.lib.pl_debug_set_plan_device(plan.handle, 0) == _native.PL_EUNSUPPORTED
+    D = _native.load_diag()
+    if D is None:
+        pytest.skip("diagnostic library not built (make -C polarcode_and_ldpc_amd/csrc diag)")
+    h = ctypes.c_void_p()
+    assert D.pl_polar_plan_create(N, K, mask.ctypes.data_as(ctypes.c_void_p), L, 0, ctypes.byref(h)) == 0
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P_ = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    ws = torch.empty(plan.workspace_bytes(B), dtype=torch.uint8, device="cuda")
+    cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
     cur = torch.cuda.current_device()
-    _native.check(_native.lib.pl_debug_set_plan_device(plan.handle, cur + 7), "set device")
-    for call in (lambda: plan.decode(llr, c), lambda: plan.reserve(B), lambda: plan.set_crc(8, 0x1D),
-                 lambda: plan.decode(llr, c, ws=torch.empty(plan.workspace_bytes(B), dtype=torch.uint8,
-                                                              device="cuda")),
-                 lambda: _native.polar_encode(plan, a, torch.empty((B, N), dtype=torch.uint8, device="cuda"))):
-        with pytest.raises(AssertionError, match="not the plan's device"):
-            call()
-    assert plan.workspace_stats() == (0, 0)  # nothing was allocated on the wrong device
-    _native.check(_native.lib.pl_debug_set_plan_device(plan.handle, cur), "set device")
+    assert D.pl_debug_set_plan_device(h, cur + 7) == 0
+    calls = {
+        "pl_decode": lambda: D.pl_decode(h, P_(llr), B, N, P_(c), None, st),
+        "pl_plan_reserve": lambda: D.pl_plan_reserve(h, B, st),
+        "pl_plan_release": lambda: D.pl_plan_release(h, st),
+        "pl_polar_plan_set_crc": lambda: D.pl_polar_plan_set_crc(h, 8, 0x1D),
+        "pl_decode_ws": lambda: D.pl_decode_ws(h, P_(llr), B, N, P_(c), None, P_(ws), ws.numel(), st),
+        "pl_polar_encode": lambda: D.pl_polar_encode(h, P_(a), B, P_(cw), st),
+    }
+    for name, call in calls.items():
+        assert call() == _native.PL_EINVAL, name
+        assert b"not the plan's device" in D.pl_last_error(), name
+    n_, b_ = ctypes.c_int64(), ctypes.c_int64()
+    assert D.pl_plan_workspace_stats(h, ctypes.byref(n_), ctypes.byref(b_)) == 0
+    assert (n_.value, b_.value) == (0, 0)  # nothing was allocated on the wrong device
+    assert D.pl_debug_set_plan_device(h, cur) == 0
     c.zero_()
-    plan.decode(llr, c)
+    assert D.pl_decode(h, P_(llr), B, N, P_(c), None, st) == 0
     torch.cuda.synchronize()
     assert torch.equal(a, c)
+    assert D.pl_plan_destroy(h) == 0
 
 
 def test_caller_workspace_and_lazy_sizing(gpu):

@@ -29,7 +29,8 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_SO) or os.path.getmtime(_SO) < os.path.getmtime(os.path.join(_HERE, "refcpu.c")):
+        srcs = [os.path.join(_HERE, f) for f in ("refcpu.c", "pysort.h")]
+        if not os.path.exists(_SO) or os.path.getmtime(_SO) < max(os.path.getmtime(f) for f in srcs):
             build()
         L = ctypes.CDLL(_SO)
         P = ctypes.c_void_p
@@ -42,6 +43,7 @@ def lib():
                                              ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
         L.orc_crc.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
         L.orc_crc.restype = ctypes.c_uint32
+        L.orc_pysort_desc.argtypes = [P, ctypes.c_int, P]
         _lib = L
     return _lib
 
@@ -120,3 +122,13 @@ def ldpc_decode(row_ptr, col_idx, n, llr, algo="bp", max_iter=20, early_stop=Tru
 def crc(bits, crc_len, poly):
     b = np.ascontiguousarray(np.asarray(bits, np.uint8))
     return lib().orc_crc(_ptr(b), len(b), crc_len, poly)
+
+
+def pysort_desc(keys):
+    """Permutation that CPython 3.10's list.sort(key=..., reverse=True) applies to
+    a list whose keys are `keys` (float64, NaN allowed): oracle/pysort.h."""
+    k = np.ascontiguousarray(np.asarray(keys, np.float64))
+    perm = np.zeros(len(k), np.int32)
+    if lib().orc_pysort_desc(_ptr(k), len(k), _ptr(perm)):
+        raise RuntimeError("oracle pysort failed")
+    return perm

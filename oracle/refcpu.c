@@ -14,7 +14,9 @@
  * Every function mirrors the reference data layout and loop order:
  *   SC   : src/polar/decoder.py:38-170   (L,B matrices of shape N x (n+1))
  *   SCL  : src/polar/decoder.py:225-441  (per-path L/B, full snapshot copies,
- *                                          stable descending sort, argmax)
+ *                                          CPython's list.sort order (pysort.h:
+ *                                          stable descending for finite metrics,
+ *                                          exact for NaN ones), np.argmax)
  *   BP   : src/ldpc/decoder.py:62-202    (flooding, tanh rule, clip +-0.999999)
  *   MS   : src/ldpc/decoder.py:257-352
  * Arithmetic dependencies: NumPy ufuncs in the reference -> libm here
@@ -27,6 +29,7 @@
 #ifdef _OPENMP
 #include <omp.h>
 #endif
+#include "pysort.h" /* CPython 3.10 list.sort restated (NaN metrics) */
 
 #define ORC_OK 0
 #define ORC_EINVAL -1
@@ -149,8 +152,12 @@ static int scl_decode_impl(int N, int Lsz, const uint8_t* frozen_mask, const dou
     uint8_t* act = (uint8_t*)malloc(Lsz);
     cand_t* cand = (cand_t*)malloc(sizeof(cand_t) * 2 * Lsz);
     int* aidx = (int*)malloc(sizeof(int) * Lsz);
-    if (!Lp || !Bp || !oL || !oB || !pm || !act || !cand || !aidx) {
+    cand_t* cand2 = (cand_t*)malloc(sizeof(cand_t) * 2 * Lsz);
+    ps_item* srt = (ps_item*)malloc(sizeof(ps_item) * 2 * Lsz);
+    ps_item* stmp = (ps_item*)malloc(sizeof(ps_item) * (Lsz + 1));
+    if (!Lp || !Bp || !oL || !oB || !pm || !act || !cand || !aidx || !cand2 || !srt || !stmp) {
         free(Lp); free(Bp); free(oL); free(oB); free(pm); free(act); free(cand); free(aidx);
+        free(cand2); free(srt); free(stmp);
         return ORC_ENOMEM;
     }
     for (size_t k = 0; k < per * Lsz; k++) { Lp[k] = NAN; Bp[k] = NAN; }
@@ -204,14 +211,14 @@ static int scl_decode_impl(int N, int Lsz, const uint8_t* frozen_mask, const dou
                 cand[a].m = pm[p] + log_likelihood(lv, 0); cand[a].p = p; cand[a].bit = 0;
                 cand[na + a].m = pm[p] + log_likelihood(lv, 1); cand[na + a].p = p; cand[na + a].bit = 1;
             }
-            /* list.sort(key=metric, reverse=True): stable, equal keys keep order */
+            /* all_candidates.sort(key=lambda x: x[0], reverse=True) (:306-307): CPython's
+             * algorithm (pysort.h) -- stable descending for finite metrics, and the
+             * interpreter's own order when NaN metrics compare false both ways */
             const int nc = 2 * na;
-            for (int a = 1; a < nc; a++) {
-                cand_t x = cand[a];
-                int b = a - 1;
-                while (b >= 0 && cand[b].m < x.m) { cand[b + 1] = cand[b]; b--; }
-                cand[b + 1] = x;
-            }
+            for (int a = 0; a < nc; a++) { srt[a].k = cand[a].m; srt[a].v = a; }
+            ps_sort_desc(srt, nc, stmp);
+            for (int a = 0; a < nc; a++) cand2[a] = cand[srt[a].v];
+            memcpy(cand, cand2, sizeof(cand_t) * nc);
             const int ns = nc < Lsz ? nc : Lsz;
             memcpy(oL, Lp, sizeof(double) * per * Lsz);                  /* :314-316 */
             memcpy(oB, Bp, sizeof(double) * per * Lsz);
@@ -229,18 +236,16 @@ static int scl_decode_impl(int N, int Lsz, const uint8_t* frozen_mask, const dou
 #undef UPD_LLR
 #undef UPD_BITS
     }
-    /* np.argmax: first maximum */
+    /* np.argmax (:258): the first NaN if there is one, else the first maximum */
     int best = 0;
-    for (int p = 1; p < Lsz; p++) if (pm[p] > pm[best]) best = p;
+    for (int p = 1; p < Lsz && !isnan(pm[best]); p++) if (isnan(pm[p]) || pm[p] > pm[best]) best = p;
     if (crc_len > 0) {
+        /* build-defined CA-SCL: active paths in the order list.sort(key=metric,
+         * reverse=True) leaves them (stable descending; CPython's order with NaN) */
         int na = 0;
-        for (int p = 0; p < Lsz; p++) if (act[p]) aidx[na++] = p;
-        for (int a = 1; a < na; a++) {  /* stable sort by metric, descending */
-            const int x = aidx[a];
-            int b = a - 1;
-            while (b >= 0 && pm[aidx[b]] < pm[x]) { aidx[b + 1] = aidx[b]; b--; }
-            aidx[b + 1] = x;
-        }
+        for (int p = 0; p < Lsz; p++) if (act[p]) { srt[na].k = pm[p]; srt[na].v = p; na++; }
+        ps_sort_desc(srt, na, stmp);
+        for (int a = 0; a < na; a++) aidx[a] = srt[a].v;
         uint8_t* msg = (uint8_t*)malloc((size_t)N);
         for (int a = 0; a < na && msg; a++) {
             int k = 0;
@@ -253,6 +258,19 @@ static int scl_decode_impl(int N, int Lsz, const uint8_t* frozen_mask, const dou
 #undef PL
 #undef PB
     free(Lp); free(Bp); free(oL); free(oB); free(pm); free(act); free(cand); free(aidx);
+    free(cand2); free(srt); free(stmp);
+    return ORC_OK;
+}
+
+/* test hook: the permutation list.sort(key=k, reverse=True) applies (pysort.h) */
+int orc_pysort_desc(const double* keys, int n, int32_t* perm) {
+    ps_item* a = (ps_item*)malloc(sizeof(ps_item) * (size_t)(n > 0 ? n : 1));
+    ps_item* t = (ps_item*)malloc(sizeof(ps_item) * (size_t)(n / 2 + 1));
+    if (!a || !t) { free(a); free(t); return ORC_ENOMEM; }
+    for (int i = 0; i < n; i++) { a[i].k = keys[i]; a[i].v = i; }
+    ps_sort_desc(a, n, t);
+    for (int i = 0; i < n; i++) perm[i] = a[i].v;
+    free(a); free(t);
     return ORC_OK;
 }
 

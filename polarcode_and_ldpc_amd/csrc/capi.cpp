@@ -63,6 +63,11 @@ struct pl_plan {
     // frame), one buffer per stream (plans are shared across host threads that
     // use distinct streams; a decode only ever touches its stream's buffer)
     size_t ws_unit = 0;
+    // polar list decoders: NaN-frame masks (kNanMaskPasses u64 per resident
+    // wavefront, at the start of the workspace) and the scratch one workgroup of
+    // polar_nan_redo_kernel needs (it reuses the list kernel's slices after it)
+    size_t mask_bytes = 0, redo_unit = 0;
+    int redo_blocks = 0;
     std::mutex mu;  // guards the map only; each entry has its own mutex
     std::unordered_map<hipStream_t, std::shared_ptr<Workspace>> ws;
 };
@@ -209,6 +214,16 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
     p->lane_grid_max = per_cu * device_cus(p->device);
     const int waves_env = env_int("PL_POLAR_WAVES", 0);
     if (waves_env > 0) p->lane_grid_max = waves_env;
+    if (!p->sc) {
+        p->mask_bytes = pl::nan_mask_region(p->lane_grid_max);
+        p->redo_unit = pl::nan_redo_unit(N, list_size);
+        p->redo_blocks = device_cus(p->device);
+        // the kernel's dynamic-LDS limit is per function: set it for the largest list once
+        if ((e = pl::nan_redo_prepare(1024)) != hipSuccess) {
+            pl_plan_destroy(p);
+            return hipfail(e, "NaN redo kernel prepare");
+        }
+    }
     *out = p;
     return PL_OK;
 }
@@ -351,12 +366,22 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     return PL_OK;
 }
 
+// Polar workspace layout for a grid of `grid` resident wavefronts: a list
+// plan's NaN masks first (for its largest grid, so they stay in place, and
+// zero, from one decode to the next), then the list kernel's slices, which the
+// NaN redo kernel reuses as its scratch once the list kernel is done.
+static size_t polar_bytes(const pl_plan* p, int64_t grid) {
+    return p->mask_bytes + std::max<size_t>(p->ws_unit * (size_t)grid, p->redo_unit);
+}
+// the smallest workspace a decode can run on (one wavefront's slice)
+static size_t ws_min(const pl_plan* p) { return p->kind == 0 ? polar_bytes(p, 1) : p->ws_unit; }
+
 // Workspace bytes a decode of `batch` frames uses at full speed.
 static size_t ws_need(const pl_plan* p, int64_t batch) {
-    if (batch <= 0 || p->ws_unit == 0) return 0;
+    if (batch <= 0 || (p->ws_unit == 0 && p->redo_unit == 0)) return 0;
     if (p->kind == 0) {
         const int64_t waves = (batch + p->fpw - 1) / p->fpw;
-        return p->ws_unit * (size_t)std::min<int64_t>(waves, p->lane_grid_max);
+        return polar_bytes(p, std::min<int64_t>(waves, p->lane_grid_max));
     }
     return p->ws_unit * (size_t)std::min<int64_t>(batch, p->ldpc_chunk);
 }
@@ -364,23 +389,46 @@ static size_t ws_need(const pl_plan* p, int64_t batch) {
 // Decode with an explicit workspace of ws_bytes (>= one unit when one is needed):
 // the polar grid / LDPC chunk is clamped to what the workspace holds.
 static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits, int32_t* iters,
-                       void* ws, size_t ws_bytes, unsigned long long* stamps, hipStream_t s) {
-    if (p->ws_unit > 0 && (ws == nullptr || ws_bytes < p->ws_unit))
+                       void* ws, size_t ws_bytes, unsigned long long* stamps, hipStream_t s, bool zero_masks = false) {
+    const size_t wmin = ws_min(p);
+    if (wmin > 0 && (ws == nullptr || ws_bytes < wmin))
         return fail(PL_EINVAL, "workspace smaller than one unit (pl_plan_workspace_bytes)");
     if (p->kind == 0) {
+        if (!p->tree && stamps) return fail(PL_EUNSUPPORTED, "stamps only for the tree kernel");
         const int64_t waves = (batch + p->fpw - 1) / p->fpw;
-        const int64_t fit = (int64_t)(ws_bytes / p->ws_unit);
-        const int grid = (int)std::min<int64_t>(std::min<int64_t>(waves, p->lane_grid_max), fit);
-        hipError_t e;
-        if (p->tree)
-            e = pl::tree_launch(p->tinfo, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, p->pg.K,
-                                p->sc ? 1 : p->list_size, (unsigned char*)ws, grid, stamps, p->d_crc_g, p->d_r0k, s);
-        else if (stamps)
-            return fail(PL_EUNSUPPORTED, "stamps only for the tree kernel");
-        else
-            e = pl::lane_launch(p->lgeo, p->sc, llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch,
-                                (unsigned char*)ws, grid, p->d_crc_g, s);
-        return e == hipSuccess ? PL_OK : hipfail(e, "polar decode launch");
+        int64_t grid = std::min<int64_t>(waves, p->lane_grid_max);
+        while (grid > 1 && polar_bytes(p, grid) > ws_bytes) grid = std::min<int64_t>(grid - 1, grid * ws_bytes / polar_bytes(p, grid));
+        unsigned char* const base = (unsigned char*)ws;
+        uint64_t* const masks = p->mask_bytes ? (uint64_t*)base : nullptr;
+        unsigned char* const slices = base + p->mask_bytes;
+        if (masks && zero_masks) {  // a caller-owned workspace: the masks may hold anything
+            hipError_t e = hipMemsetAsync(masks, 0, (size_t)grid * 8 * pl::kNanMaskPasses, s);
+            if (e != hipSuccess) return hipfail(e, "NaN mask reset");
+        }
+        // a list launch runs at most kNanMaskPasses passes of its grid (the masks' depth)
+        const int64_t step = masks ? grid * p->fpw * pl::kNanMaskPasses : batch;
+        for (int64_t b0 = 0; b0 < batch; b0 += step) {
+            const int64_t nb = std::min<int64_t>(step, batch - b0);
+            const double* l0 = llr + b0 * ld;
+            uint8_t* o0 = bits + b0 * p->pg.K;
+            hipError_t e;
+            if (p->tree)
+                e = pl::tree_launch(p->tinfo, l0, ld, o0, p->d_frozen_dec, p->d_info_pos, nb, p->pg.K,
+                                    p->sc ? 1 : p->list_size, slices, (int)grid, stamps, p->d_crc_g,
+                                    p->sc ? (const void*)p->d_r0k : (const void*)masks, s);
+            else
+                e = pl::lane_launch(p->lgeo, p->sc, l0, ld, o0, p->d_frozen_dec, p->d_info_pos, nb, slices, (int)grid,
+                                    p->d_crc_g, masks, s);
+            if (e != hipSuccess) return hipfail(e, "polar decode launch");
+            if (masks) {
+                // frames whose list saw a NaN metric, in the reference's candidate order
+                e = pl::nan_redo_launch(l0, ld, o0, nb, p->pg.N, p->pg.K, p->list_size, p->d_frozen_dec,
+                                        p->d_info_pos, p->d_crc_g, masks, (int)grid, p->fpw, slices,
+                                        ws_bytes - p->mask_bytes, p->redo_blocks, s);
+                if (e != hipSuccess) return hipfail(e, "polar NaN redo launch");
+            }
+        }
+        return PL_OK;
     }
     if (!p->lg.use_global) {
         // one workgroup per frame; HIP caps a grid at 2^32 work-items
@@ -421,7 +469,7 @@ static std::shared_ptr<Workspace> stream_entry(pl_plan* p, hipStream_t s) {
 static int grow_ws(pl_plan* p, Workspace* w, hipStream_t s, size_t need, bool retry) {
     if (w->bytes >= need) return PL_OK;
     if (!retry && w->ptr && w->failed_need && need <= w->failed_need) return PL_OK;  // fell back for this size
-    const size_t unit = std::max<size_t>(p->ws_unit, 1);
+    const size_t unit = std::max<size_t>(ws_min(p), 1);
     size_t want = need;
     for (;;) {
         void* np = nullptr;
@@ -441,6 +489,10 @@ static int grow_ws(pl_plan* p, Workspace* w, hipStream_t s, size_t need, bool re
             w->ptr = np;
             w->bytes = want;
             w->failed_need = want < need ? need : 0;
+            if (p->mask_bytes) {  // NaN masks start at zero (the decodes keep them so)
+                hipError_t me = hipMemsetAsync(np, 0, p->mask_bytes, s);
+                if (me != hipSuccess) return hipfail(me, "NaN mask reset");
+            }
             return PL_OK;
         }
         (void)hipGetLastError();  // clear the sticky allocation error before retrying
@@ -544,7 +596,7 @@ extern "C" int pl_decode_ws(pl_plan* p, const double* llr, int64_t batch, int64_
     if (workspace_bytes < 0) return fail(PL_EINVAL, "workspace_bytes < 0");
     if ((rc = check_device(p))) return rc;
     return decode_impl(p, llr, batch, ld, bits, iters, workspace, (size_t)workspace_bytes, nullptr,
-                       (hipStream_t)stream);
+                       (hipStream_t)stream, true);
 }
 
 extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,

@@ -32,7 +32,7 @@ int lane_geom(int N, int K, int list_size, int F, int lds_budget, LaneGeom* g);
 hipError_t lane_prepare(const LaneGeom& g, bool sc, int* max_blocks_per_cu);
 hipError_t lane_launch(const LaneGeom& g, bool sc, const double* llr, int64_t ld, uint8_t* out,
                        const uint32_t* frozen_dec, const int32_t* info_pos, int64_t batch, unsigned char* ws,
-                       int grid, const uint32_t* crc_g, hipStream_t s);
+                       int grid, const uint32_t* crc_g, uint64_t* nan_masks, hipStream_t s);
 
 // v4 lane-per-path decoder with compile-time geometry (polar_tree.hip); built
 // for the (n, list capacity) pairs in its table, polar_lane.hip covers the rest.
@@ -47,8 +47,25 @@ bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info);
 hipError_t tree_prepare(const TreeInfo& t, int* max_blocks_per_cu);
 hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t* out, const uint32_t* frozen_dec,
                        const int32_t* info_pos, int64_t batch, int K, int Lsz, unsigned char* ws, int grid,
-                       unsigned long long* stamps, const uint32_t* crc_g, const uint32_t* r0k, hipStream_t s);
+                       unsigned long long* stamps, const uint32_t* crc_g, const void* aux, hipStream_t s);
 
+// SCL frames with NaN path metrics (polar_nan.hip): the list kernels set bit f
+// of masks[wave][pass] for frame f of that pass; polar_nan_redo_kernel decodes
+// those frames again in the reference's candidate order.  A launch runs at most
+// kNanMaskPasses passes of its persistent grid.
+constexpr int kNanMaskPasses = 64;
+// Bytes of the mask words of up to `grid` wavefronts, u64 [grid][kNanMaskPasses]
+// (a multiple of 64 KB, at the start of a list plan's workspace).  They are zero
+// between decodes: zeroed when the workspace is allocated, ORed by the list
+// kernels, re-zeroed by the redo kernel after it reads them.
+inline size_t nan_mask_region(int64_t grid) { return ((size_t)grid * 8 * kNanMaskPasses + 65535) / 65536 * 65536; }
+size_t nan_redo_unit(int N, int list_size);  // scratch bytes per redo workgroup
+int nan_redo_lds_bytes(int list_size);
+hipError_t nan_redo_prepare(int list_size);
+hipError_t nan_redo_launch(const double* llr, int64_t ld, uint8_t* out, int64_t batch, int N, int K, int Lsz,
+                           const uint32_t* frozen_dec, const int32_t* info_pos, const uint32_t* crc_g,
+                           uint64_t* masks, int grid, int fpw, unsigned char* scratch, size_t scratch_bytes,
+                           int max_blocks, hipStream_t s);
 
 hipError_t polar_encode_launch(int N, int K, const int32_t* pos2info, const uint8_t* msg,
                                int64_t batch, uint8_t* cw, hipStream_t s);

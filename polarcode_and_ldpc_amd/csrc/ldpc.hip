@@ -465,6 +465,60 @@ PL_DEV double ms_c2v(double2 mm, uint32_t meta, int i, double norm) {
     return sp * mn * norm;
 }
 
+#ifndef PL_MS_CB
+#define PL_MS_CB 2  // regular codes: checks whose loads are issued together in the check pass
+#endif
+#ifndef PL_MS_VB
+#define PL_MS_VB 2  // regular codes: variables whose state loads are issued together
+#endif
+
+// All DC outputs of a check from its state, equal to ms_c2v position by
+// position: with no zero and no NaN input (the usual case) the sign product is
+// +-1, so (sp * mn) * norm = +-(mn * norm) -- two multiplies per check instead
+// of one per position (rounding is sign-symmetric).
+template <int DC>
+PL_DEV void ms_c2v_all(double2 mm, uint32_t meta, double norm, double* out) {
+    if ((meta & 0x0C30u) == 0u) {
+        const double a1 = mm.x * norm, a2 = mm.y * norm;
+        const int idx1 = (int)(meta & 15u);
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const double mag = k == idx1 ? a2 : a1;
+            const uint64_t sgn = (uint64_t)(((meta >> 16) ^ (meta >> (17 + k))) & 1u) << 63;
+            out[k] = __longlong_as_double((long long)((uint64_t)__double_as_longlong(mag) ^ sgn));
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < DC; ++k) out[k] = ms_c2v(mm, meta, k, norm);
+    }
+}
+
+// Check-state update from a check's DC inputs x_k (min-sum statistics, see
+// ms_c2v); syndrome of the decisions rides along in `s`.
+template <int DC>
+PL_DEV void ms_state(const double* x, double2& mm, uint32_t& meta) {
+    double min1 = __builtin_inf(), min2 = __builtin_inf();
+    uint32_t idx1 = 0, ncnt = 0, nidx = 0, zcnt = 0, zidx = 0, par = 0, negs = 0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        if (__builtin_isnan(x[k])) {
+            if (ncnt == 0) nidx = (uint32_t)k;
+            ncnt = ncnt < 2 ? ncnt + 1 : 2;
+        } else {
+            const double a = fabs(x[k]);
+            if (a < min1) { min2 = min1; min1 = a; idx1 = (uint32_t)k; }
+            else if (a < min2) min2 = a;
+        }
+        if (x[k] == 0.0) {
+            if (zcnt == 0) zidx = (uint32_t)k;
+            zcnt = zcnt < 2 ? zcnt + 1 : 2;
+        }
+        if (x[k] < 0.0) { par ^= 1u; negs |= 1u << k; }
+    }
+    mm = make_double2(min1, min2);
+    meta = idx1 | (ncnt << 4) | (nidx << 6) | (zcnt << 10) | (zidx << 12) | (par << 16) | (negs << 17);
+}
+
 // One workgroup (1024 threads) per frame.  Per iteration: check pass (thread =
 // check: v2c_k = total[v_k] - c2v_k(old state) as decoder.py:120 forms it --
 // llr itself at iteration 0 -- new state in place, syndrome of the decisions of
@@ -529,6 +583,53 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
     int done = g.max_iter;
     for (int it = 0; it < g.max_iter; ++it) {
         int syn = 0;
+        if constexpr (RI && DV > 0 && DV < 8 && PL_MS_CB > 0) {
+            // regular code, indices in registers: the loads of PL_MS_CB checks
+            // (their old state and DC totals) issue before any of them is
+            // reduced (a store to the state would otherwise order every later
+            // load behind it); same arithmetic as the loop below
+            constexpr int CB = PL_MS_CB < MQ ? (PL_MS_CB > 0 ? PL_MS_CB : 1) : MQ;
+#pragma unroll
+            for (int q0 = 0; q0 < MQ; q0 += CB) {
+                double2 om[CB];
+                uint32_t ometa[CB];
+                double tv[CB][DC];
+#pragma unroll
+                for (int b = 0; b < CB; ++b) {
+                    const int c = tid + 1024 * (q0 + b);
+                    const bool ok = q0 + b < MQ && c < m;
+                    om[b] = ok ? smin[c] : make_double2(0.0, 0.0);
+                    ometa[b] = ok ? smeta[c] : 0u;
+#pragma unroll
+                    for (int k = 0; k < DC; ++k)
+                        tv[b][k] = ok ? tot[(int)((ccol[(q0 + b) < MQ ? q0 + b : 0][k >> 1] >> (16 * (k & 1))) & 0xFFFFu)] : 1.0;
+                }
+#pragma unroll
+                for (int b = 0; b < CB; ++b) {
+                    const int c = tid + 1024 * (q0 + b);
+                    if (q0 + b >= MQ || c >= m) continue;
+                    double x[DC];
+                    int sp = 0;
+                    if (it == 0) {
+#pragma unroll
+                        for (int k = 0; k < DC; ++k) x[k] = tv[b][k];
+                    } else {
+                        double c2v[DC];
+                        ms_c2v_all<DC>(om[b], ometa[b], g.norm, c2v);
+#pragma unroll
+                        for (int k = 0; k < DC; ++k) x[k] = tv[b][k] - c2v[k];
+                    }
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) sp ^= (tv[b][k] <= 0.0) ? 1 : 0;
+                    syn |= sp;
+                    double2 mm;
+                    uint32_t meta;
+                    ms_state<DC>(x, mm, meta);
+                    smin[c] = mm;
+                    smeta[c] = meta;
+                }
+            }
+        } else {
 #pragma unroll
         for (int q = 0; q < (RI ? MQ : 1); ++q)
         for (int c = tid + 1024 * q; c < m; c += (RI ? m : nt)) {
@@ -569,11 +670,44 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
             smin[c] = make_double2(min1, min2);
             smeta[c] = idx1 | (ncnt << 4) | (nidx << 6) | (zcnt << 10) | (zidx << 12) | (par << 16) | (negs << 17);
         }
+        }
         if (g.early_stop && it > 0) {
             if (!__syncthreads_or(syn)) { done = it; break; }
         } else {
             __syncthreads();
         }
+        if constexpr (RI && DV > 0 && DV < 8 && PL_MS_VB > 0) {
+            // regular code: the state loads of PL_MS_VB variables issue together
+            constexpr int VB = PL_MS_VB < VPT ? (PL_MS_VB > 0 ? PL_MS_VB : 1) : VPT;
+#pragma unroll
+            for (int j0 = 0; j0 < VPT; j0 += VB) {
+                double2 mm[VB][DV];
+                uint32_t mt[VB][DV];
+                int pos[VB][DV];
+#pragma unroll
+                for (int b = 0; b < VB; ++b) {
+                    const int v = tid + 1024 * (j0 + b);
+                    const bool ok = j0 + b < VPT && v < n;
+#pragma unroll
+                    for (int k = 0; k < DV; ++k) {
+                        const int cpk = RV ? (int)((vcp[RV && (j0 + b) < VPT ? j0 + b : 0][k >> 1] >> (16 * (k & 1))) & 0xFFFFu)
+                                           : (ok ? dv.var_cp[v * DV + k] : 0);
+                        pos[b][k] = cpk & 15;
+                        mm[b][k] = ok ? smin[cpk >> 4] : make_double2(0.0, 0.0);
+                        mt[b][k] = ok ? smeta[cpk >> 4] : 0u;
+                    }
+                }
+#pragma unroll
+                for (int b = 0; b < VB; ++b) {
+                    const int v = tid + 1024 * (j0 + b);
+                    if (j0 + b >= VPT || v >= n) continue;
+                    double sum = 0.0;  // np.sum over DV < 8 terms: sequential
+#pragma unroll
+                    for (int k = 0; k < DV; ++k) sum += ms_c2v(mm[b][k], mt[b][k], pos[b][k], g.norm);
+                    tot[v] = chv[j0 + b] + sum;
+                }
+            }
+        } else {
 #pragma unroll
         for (int jv = 0; jv < (VPT > 0 ? VPT : 1); ++jv) {
           for (int v = tid + 1024 * jv; v < n; v += (VPT > 0 ? n : nt)) {
@@ -610,6 +744,7 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
             }
             tot[v] = (VPT > 0 ? chv[jv] : ch[v]) + sum;
           }
+        }
         }
         __syncthreads();
     }

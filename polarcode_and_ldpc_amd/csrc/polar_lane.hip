@@ -87,12 +87,12 @@ hipError_t lane_prepare(const LaneGeom& g, bool sc, int* max_blocks_per_cu) {
 
 hipError_t lane_launch(const LaneGeom& g, bool sc, const double* llr, int64_t ld, uint8_t* out,
                        const uint32_t* frozen_dec, const int32_t* info_pos, int64_t batch, unsigned char* ws,
-                       int grid, const uint32_t* crc_g, hipStream_t s) {
+                       int grid, const uint32_t* crc_g, uint64_t* nan_masks, hipStream_t s) {
     void* k = lane_kernel(g, sc);
     if (!k) return hipErrorInvalidValue;
     LaneGeom gg = g;
-    void* args[] = {&gg, (void*)&llr, (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos, (void*)&batch,
-                    (void*)&ws, (void*)&crc_g};
+    void* args[] = {&gg,           (void*)&llr,   (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos,
+                    (void*)&batch, (void*)&ws,    (void*)&crc_g, (void*)&nan_masks};
     return hipLaunchKernel(k, dim3((unsigned)grid), dim3((unsigned)g.lw), args, g.lds_bytes, s);
 }
 

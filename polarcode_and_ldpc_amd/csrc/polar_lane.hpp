@@ -211,7 +211,8 @@ template <int LCAP, bool SC, int F, int B>
 __global__ void __launch_bounds__(LCAP > 64 ? LCAP : 64)
 polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_t* __restrict__ out,
                   const uint32_t* __restrict__ frozen_dec, const int32_t* __restrict__ info_pos, int64_t batch,
-                  unsigned char* __restrict__ workspace, const uint32_t* __restrict__ crc_g) {
+                  unsigned char* __restrict__ workspace, const uint32_t* __restrict__ crc_g,
+                  uint64_t* __restrict__ nan_masks) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int FPW = LCAP >= 64 ? 1 : 64 / LCAP;
     constexpr int LW = LCAP > 64 ? LCAP : 64;  // lanes per workgroup
@@ -228,10 +229,12 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
     c.base = fw * LCAP;
     c.lw = LW;
 
-    for (int64_t f0 = (int64_t)blockIdx.x * FPW; f0 < batch; f0 += (int64_t)gridDim.x * FPW) {
+    int pass = 0;
+    for (int64_t f0 = (int64_t)blockIdx.x * FPW; f0 < batch; f0 += (int64_t)gridDim.x * FPW, ++pass) {
         const int64_t frame = f0 + fw;
         const bool live = frame < batch;
         const double* __restrict__ ch = llr + (live ? frame : batch - 1) * ld;
+        bool nanf = false;  // a NaN candidate / final metric: redone by polar_nan.hip
         Row row;
 #pragma unroll
         for (int k = 0; k < Row::NW; ++k) row.a[k] = row.b[k] = (uint64_t)(uint32_t)slot * Row::REP;
@@ -294,6 +297,7 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
             } else {
                 double m0, m1;
                 path_metrics<true>(pm, lam, m0, m1);
+                nanf |= (slot < nact) & (__builtin_isnan(m0) | __builtin_isnan(m1));
                 const int nsurv = (2 * nact < g.Lsz) ? 2 * nact : g.Lsz;
               if constexpr (LCAP > 64) {
                 // the same ranks through LDS: publish (m0, m1) and the pointer
@@ -442,6 +446,23 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
 
         // ------------------------------------------------ best path, output
         int best = 0;
+        if constexpr (!SC) {
+            nanf |= (slot < nact) & __builtin_isnan(pm);
+            if constexpr (LCAP > 64) {
+                const bool any = __syncthreads_or(nanf);
+                if (nan_masks && pass < kNanMaskPasses && lane == 0)
+                    nan_masks[(size_t)blockIdx.x * kNanMaskPasses + pass] = any ? 1ull : 0ull;
+            } else {
+                const uint64_t bal = __ballot(nanf);
+                if (nan_masks && pass < kNanMaskPasses) {
+                    constexpr uint64_t GM = LCAP >= 64 ? ~0ull : ((1ull << LCAP) - 1ull);
+                    uint64_t fm = 0;
+#pragma unroll
+                    for (int f = 0; f < FPW; ++f) fm |= (uint64_t)(((bal >> (f * LCAP)) & GM) != 0ull) << f;
+                    if (lane == 0) nan_masks[(size_t)blockIdx.x * kNanMaskPasses + pass] = fm;
+                }
+            }
+        }
         if constexpr (!SC && LCAP > 64) {
             double* const xp = reinterpret_cast<double*>(smem + g.lds_xchg);
             uint32_t* const xkey = reinterpret_cast<uint32_t*>(xp + LW);

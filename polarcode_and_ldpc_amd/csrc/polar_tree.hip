@@ -624,7 +624,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restrict__ out,
                   const uint32_t* __restrict__ frozen_dec, const int32_t* __restrict__ info_pos, int64_t batch,
                   int K, int Lsz, unsigned char* __restrict__ workspace, unsigned long long* __restrict__ stamps,
-                  const uint32_t* __restrict__ crc_g, const uint32_t* __restrict__ r0k) {
+                  const uint32_t* __restrict__ crc_g, const uint32_t* __restrict__ aux) {
+    // aux: SC -- the rate-0 node table r0k; lists -- the NaN mask words,
+    // u64 [gridDim.x][kNanMaskPasses], zero on entry (polar_nan.hip re-zeroes the
+    // words it reads).  One argument for both: a separate mask pointer kept live
+    // across the leaf loop cost the list instances 8-24 spilled bytes per lane.
+    const uint32_t* __restrict__ r0k = SC ? aux : nullptr;
     using G = TG<NL, LCAP, F, DL>;
     constexpr int n = G::n, N = G::N, FPW = G::FPW;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -678,12 +683,22 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 raw = reinterpret_cast<const double2*>(row) + lane / FPW;
             constexpr int CV = 2 << G::NS;    // channel values per lane per step
             constexpr int CPI = 64 / FPW;     // chunks per frame per step
+            // NaN path metrics need a NaN LLR at a leaf, i.e. a NaN input or an
+            // inf - inf in a g; with every |input| < 2^1000 (and none NaN) each of
+            // the <= 12 levels at most doubles a magnitude, so every LLR is finite
+            // and every metric a sum of finite non-positive terms (-inf at worst,
+            // never NaN).  Frames with a NaN or |input| >= 2^1000 are flagged in
+            // this pass's mask word (aux) and decoded again by polar_nan.hip in the
+            // reference's exact candidate order (list.sort, decoder.py:306-307).
+            bool ext = false;
 #pragma unroll 1
             for (int cb = 0; cb < N / CV; cb += CPI) {
                 const int cc = cb + lane / FPW;
                 double v[CV];
 #pragma unroll
                 for (int k = 0; k < CV; ++k) v[k] = row[CV * cc + k];
+#pragma unroll
+                for (int k = 0; k < CV; ++k) ext |= !(fabs(v[k]) < 0x1p1000);
                 // depth d of the chunk: CV >> d values = CV >> (d+1) pairs
 #pragma unroll
                 for (int d = 0; d <= G::NS; ++d) {
@@ -698,6 +713,17 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                         for (int k = 0; k < np; ++k) v[k] = f_ms(v[2 * k], v[2 * k + 1]);
                     }
                 }
+            }
+            const uint64_t bal = __ballot(ext);  // lane l stages frame l % FPW
+            if (!SC && bal) {
+                uint64_t fm = 0;
+#pragma unroll
+                for (int sft = 0; sft < 64; sft += FPW) fm |= (bal >> sft) & ((1ull << FPW) - 1ull);
+                const uint32_t ps = ((uint32_t)f0 / FPW - blockIdx.x) / gridDim.x;  // pass (< 2^31 frames per launch)
+                if (lane == 0 && ps < (uint32_t)kNanMaskPasses)
+                    atomicOr(reinterpret_cast<unsigned long long*>(const_cast<uint32_t*>(aux)) +
+                                 (size_t)blockIdx.x * kNanMaskPasses + ps,
+                             (unsigned long long)fm);
             }
         }
         uint64_t lrow = G::SHADOW ? 0 : own, brow = lrow;  // shadows start on slot 0's rows
@@ -1259,9 +1285,9 @@ hipError_t tree_prepare(const TreeInfo& t, int* max_blocks_per_cu) {
 
 hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t* out, const uint32_t* frozen_dec,
                        const int32_t* info_pos, int64_t batch, int K, int Lsz, unsigned char* ws, int grid,
-                       unsigned long long* stamps, const uint32_t* crc_g, const uint32_t* r0k, hipStream_t s) {
+                       unsigned long long* stamps, const uint32_t* crc_g, const void* aux, hipStream_t s) {
     void* args[] = {(void*)&llr, (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos, (void*)&batch,
-                    (void*)&K, (void*)&Lsz, (void*)&ws, (void*)&stamps, (void*)&crc_g, (void*)&r0k};
+                    (void*)&K,   (void*)&Lsz, (void*)&ws, (void*)&stamps,     (void*)&crc_g,    (void*)&aux};
     if (stamps && !t.fn_stamps) return hipErrorInvalidValue;
     return hipLaunchKernel(stamps ? t.fn_stamps : t.fn, dim3((unsigned)grid), dim3(64), args, t.lds_bytes, s);
 }

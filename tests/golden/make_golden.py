@@ -31,6 +31,8 @@ Fixture inventory:
                            degrees are all >= 2, + BP on the same H.
   ldpc_ms_8192.npz     F7  MS-20 on an n=8192 (3,6)-regular H.
   crc.npz              F9  crc_encode vectors for CRC-8/16/24.
+  polar_nan.npz        (round 4) SCL frames with NaN path metrics (+-inf / NaN
+                           LLRs): CPython's list.sort order of NaN keys.
 """
 import argparse
 import json
@@ -501,9 +503,53 @@ def job_polar_erasures():
     return "polar_erasures.npz", out
 
 
+def job_polar_nan():
+    """SCL frames whose path metrics become NaN (round 4):
+    +-inf LLRs that meet in a g give inf - inf = NaN (decoder.py:417), the NaN
+    LLR gives NaN metrics (:374-406), and list.sort(key=..., reverse=True)
+    (:307) orders NaN keys as CPython's algorithm happens to leave them; the final
+    np.argmax (:258) picks the first NaN.  Frame kinds: BEC with +-inf and
+    erasures, all +-inf (no erasure), AWGN with 1/16 of the positions set to
+    +-inf of a random sign, AWGN with a few NaN inputs.  Lists from 1 to 64
+    (L = 32 and 64 reach CPython's merge / galloping code: 64 and 128 candidates)."""
+    polar, _, _ = _imp()
+    out = {}
+    cases = [(16, 8, (1, 2, 3, 4, 8)), (64, 32, (2, 4, 8, 16, 32, 48)), (256, 128, (4, 8, 32, 64)),
+             (1024, 512, (8, 32))]
+    for N, K, Ls in cases:
+        fr = bitrev_bhatta_frozen(N, K)
+        nfr = 12 if N <= 256 else 4
+        llr, msg, _ = _polar_frames(N, K, fr, (1.0,), nfr, 900 + N)
+        rng = np.random.RandomState(9000 + N)
+        for f in range(len(llr)):
+            kind = f % 4
+            sgn = np.where(llr[f] >= 0, 1.0, -1.0)
+            if kind == 0:
+                x = sgn * np.inf
+                x[rng.rand(N) < 0.2 + 0.3 * rng.rand()] = 0.0
+            elif kind == 1:
+                x = sgn * np.inf
+            elif kind == 2:
+                x = llr[f].copy()
+                idx = rng.choice(N, size=max(1, N // 16), replace=False)
+                x[idx] = rng.choice([np.inf, -np.inf], size=len(idx))
+            else:
+                x = llr[f].copy()
+                x[rng.choice(N, size=max(1, N // 64), replace=False)] = np.nan
+            llr[f] = x
+        out["N%d_frozen" % N] = fr
+        out["N%d_llr" % N] = llr
+        out["N%d_msg" % N] = msg
+        out["N%d_Ls" % N] = np.array(Ls)
+        for L in Ls:
+            d = polar.SCLDecoder(N, K, list_size=L, frozen_bits=fr)
+            out["N%d_L%d" % (N, L)] = np.array([d.decode(l.copy()) for l in llr])
+    return "polar_nan.npz", out
+
+
 JOBS = [job_scl4096_l8, job_scl1024_l8, job_ms8192, job_scl1024_l32, job_bp504,
         job_sc1024, job_ms504, job_small, job_p1, job_kat16, job_crc, job_ldpc_special, job_polar_erasures
-        ] + ROUND2_JOBS
+        ] + ROUND2_JOBS + [job_polar_nan]
 
 
 def _run(fn):

@@ -19,16 +19,24 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(args, timeout=300):
+def _bench(args, tmp_path, timeout=300):
+    """Run bench.py with 2 ranks; returns the full result (the --detail-out file:
+    per-rank times of every key) after checking the one compact stdout line."""
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
+    detail = str(tmp_path / "detail.json")
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
-                        "--skip-cpu"] + args, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+                        "--skip-cpu", "--detail-out", detail] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
-    return json.loads(lines[0])
+    line = json.loads(lines[0])
+    with open(detail) as f:
+        full = json.load(f)
+    assert line["value"] == pytest.approx(full["value"], rel=1e-5) and line["n_gpus"] == full["n_gpus"] == 2
+    return full
 
 
 def _ranks(d, steps, frames_per_gpu):
@@ -39,8 +47,9 @@ def _ranks(d, steps, frames_per_gpu):
     assert d["value"] > 0
 
 
-def test_bench_two_ranks_on_one_gpu(gpu):
-    r = _bench(["--sections", "polar,ldpc", "--batch", "8192", "--steps", "3", "--warmup", "1", "--snr", "0.0"])
+def test_bench_two_ranks_on_one_gpu(gpu, tmp_path):
+    r = _bench(["--sections", "polar,ldpc", "--batch", "8192", "--steps", "3", "--warmup", "1", "--snr", "0.0"],
+               tmp_path)
     assert r["n_gpus"] == 2 and len(r["rank_ms_per_step"]) == 2
     assert r["ms_per_step"] == max(r["rank_ms_per_step"])
     assert r["config"]["global_batch"] == 16384
@@ -48,11 +57,11 @@ def test_bench_two_ranks_on_one_gpu(gpu):
     assert r["value"] > 0 and r["ldpc"]["value"] > 0
 
 
-def test_bench_every_section_two_ranks(gpu):
+def test_bench_every_section_two_ranks(gpu, tmp_path):
     B, LB, steps = 4096, 2048, 2
     r = _bench(["--batch", str(B), "--long-batch", str(LB), "--steps", str(steps), "--warmup", "1",
                 "--extra-steps", str(steps), "--sweep-frames", "8192", "--sweep-max-errors", "40", "--snr", "1.0"],
-               timeout=420)
+               tmp_path, timeout=420)
     assert r["n_gpus"] == 2
     _ranks(r, steps, B)
     assert r["end_to_end"]["value"] > 0

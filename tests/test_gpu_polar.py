@@ -17,6 +17,23 @@ def _P():
     return P
 
 
+def _grid_waves(plan, fpw):
+    """Resident wavefronts of a list plan's persistent grid: the smallest batch
+    (in wavefronts) whose workspace is already the capped one."""
+    cap = plan.workspace_bytes(1 << 22)
+    hi = 1
+    while plan.workspace_bytes(hi * fpw) < cap:
+        hi *= 2
+    lo = max(1, hi // 2)
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if plan.workspace_bytes(mid * fpw) < cap:
+            lo = mid + 1
+        else:
+            hi = mid
+    return lo
+
+
 def _mismatch(a, b):
     a, b = np.asarray(a), np.asarray(b)
     assert a.shape == b.shape, (a.shape, b.shape)
@@ -538,7 +555,7 @@ def test_later_grid_passes_vs_oracle(gpu, oracle, L):
     N, K = 1024, 512
     fr = P.construct_frozen_set(N, K, 2.0)
     dec = P.SCLDecoder(N, K, L, frozen_bits=fr)
-    per_pass = dec.plan.workspace_bytes(1 << 22) // dec.plan.workspace_bytes(64 // L) * (64 // L)
+    per_pass = _grid_waves(dec.plan, 64 // L) * (64 // L)
     B = 2 * per_pass + 96  # a ragged third pass
     msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
     _native.random_bits(91, 0, msg)
@@ -673,12 +690,14 @@ def test_caller_workspace_and_lazy_sizing(gpu):
     plan = _native.polar_plan(1024, 512, mask, 8)
     unit = plan.workspace_bytes(1)
     assert unit > 0 and plan.workspace_bytes(8) == unit  # 8 frames per wave at L = 8
-    assert plan.workspace_bytes(9) == 2 * unit
+    slice_ = plan.workspace_bytes(9) - unit  # one more wavefront's slice (the NaN masks are fixed)
+    assert slice_ > 0 and plan.workspace_bytes(17) == unit + 2 * slice_
     assert plan.workspace_bytes(1 << 20) == plan.workspace_bytes(1 << 22)  # capped at the grid
     llr = torch.from_numpy(d["llr"]).cuda()
     B = llr.shape[0]
     for nunits in (1, 2, 7):
-        ws = torch.empty(nunits * unit, dtype=torch.uint8, device="cuda")
+        # garbage in the caller's buffer (NaN masks included) must not matter
+        ws = torch.full((unit + (nunits - 1) * slice_,), 0xA5, dtype=torch.uint8, device="cuda")
         out = torch.empty((B, 512), dtype=torch.uint8, device="cuda")
         plan.decode(llr, out, ws=ws)
         assert _mismatch(out.cpu().numpy(), d["scl"]) == 0, nunits
@@ -827,3 +846,106 @@ def test_sc_rate0_node_skip_vs_oracle(gpu, oracle, N, monkeypatch):
         assert dec.plan.info.reserved == 4  # the tree kernel
         got = dec.decode_batch(llr)
         assert _mismatch(got, oracle.sc_decode(N, fr, llr, threads=8)) == 0, (trial, K)
+
+
+def _nan_frames(N, K, fr, B, seed):
+    """Frames whose SCL metrics become NaN, in the four kinds of
+    make_golden.job_polar_nan (+-inf BEC with erasures, all +-inf, AWGN with
+    +-inf positions, AWGN with NaN inputs)."""
+    P = _P()
+    rng = np.random.RandomState(seed)
+    msg = rng.randint(0, 2, (B, K))
+    cw = P.PolarEncoder(N, K, frozen_bits=fr).encode_batch(msg)
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** 0.1))
+    llr = 2.0 * ((1.0 - 2.0 * cw) + sigma * rng.randn(B, N)) / sigma ** 2
+    for f in range(B):
+        kind = f % 4
+        sgn = np.where(llr[f] >= 0, 1.0, -1.0)
+        if kind == 0:
+            x = sgn * np.inf
+            x[rng.rand(N) < 0.2 + 0.3 * rng.rand()] = 0.0
+        elif kind == 1:
+            x = sgn * np.inf
+        elif kind == 2:
+            x = llr[f].copy()
+            idx = rng.choice(N, size=max(1, N // 16), replace=False)
+            x[idx] = rng.choice([np.inf, -np.inf], size=len(idx))
+        else:
+            x = llr[f].copy()
+            x[rng.choice(N, size=max(1, N // 64), replace=False)] = np.nan
+        llr[f] = x
+    return llr
+
+
+def test_scl_nan_metrics_golden(gpu):
+    """frames whose path metrics become NaN (+-inf meeting in
+    a g, decoder.py:417; NaN inputs), decoded by the reference itself
+    (make_golden.job_polar_nan).  The list kernels flag them and
+    polar_nan.hip decodes them again in CPython's list.sort order with
+    np.argmax's first NaN: bit-exact at N = 16..1024, L = 1..64 (tree and lane
+    kernels; L = 32 / 64 reach CPython's run merging and galloping)."""
+    d = golden("polar_nan.npz")
+    for N in (16, 64, 256, 1024):
+        fr, llr = d["N%d_frozen" % N], d["N%d_llr" % N]
+        K = N - len(fr)
+        for L in d["N%d_Ls" % N]:
+            dec = _P().SCLDecoder(N, K, list_size=int(L), frozen_bits=fr)
+            assert _mismatch(dec.decode_batch(llr), d["N%d_L%d" % (N, L)]) == 0, (N, L)
+
+
+@pytest.mark.parametrize("N,L,flags", [(1024, 8, 0), (1024, 32, 0), (4096, 8, 0), (256, 16, 0), (1024, 8, 0x20),
+                                       (128, 128, 0), (64, 300, 0)])
+def test_scl_nan_frames_in_large_batches(gpu, oracle, N, L, flags):
+    """NaN frames scattered over a multi-pass batch of ordinary frames: the masks
+    name the right (wavefront, pass, frame) and every other frame keeps the fast
+    kernel's bits (vs the oracle's CPython-order restatement, pinned by the
+    reference fixtures)."""
+    from polarcode_and_ldpc_amd import _native
+    P = _P()
+    K = N // 2
+    fr = P.construct_frozen_set(N, K, 2.0)
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    plan = _native.polar_plan(N, K, mask, L, flags=flags)
+    fpw = max(1, 64 // (1 << (L - 1).bit_length()))
+    B = min(2 * _grid_waves(plan, fpw) * fpw + 37, 40000 if N <= 1024 else 20000)
+    rng = np.random.RandomState(N + L)
+    msg = rng.randint(0, 2, (B, K))
+    cw = P.PolarEncoder(N, K, frozen_bits=fr).encode_batch(msg)
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** 0.15))
+    llr = 2.0 * ((1.0 - 2.0 * cw) + sigma * rng.randn(B, N)) / sigma ** 2
+    nan_idx = np.unique(np.concatenate([rng.choice(B, 24, replace=False), [0, B - 1]]))
+    llr[nan_idx] = _nan_frames(N, K, fr, len(nan_idx), seed=N * 7 + L)
+    out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    plan.decode(torch.from_numpy(llr).cuda(), out)
+    got = out.cpu().numpy().astype(np.int64)
+    chk = np.unique(np.concatenate([nan_idx, rng.choice(B, 40, replace=False)]))
+    want = oracle.scl_decode(N, L, fr, llr[chk], threads=8)
+    assert _mismatch(got[chk], want) == 0
+    # a second decode of ordinary frames on the same workspace: the masks were re-zeroed
+    clean = np.delete(np.arange(B), nan_idx)[:4096]
+    out2 = torch.empty((len(clean), K), dtype=torch.uint8, device="cuda")
+    plan.decode(torch.from_numpy(llr[clean]).cuda(), out2)
+    assert np.array_equal(out2.cpu().numpy(), got[clean])
+
+
+@pytest.mark.parametrize("N,L,crc", [(1024, 8, "CRC-8"), (1024, 32, "CRC-16"), (256, 64, "CRC-8")])
+def test_cascl_nan_frames_vs_oracle(gpu, oracle, N, L, crc):
+    """CA-SCL on NaN frames: the build-defined order of the final paths is the
+    one list.sort(key=metric, reverse=True) leaves (CPython's, with NaN keys),
+    first CRC pass, else np.argmax -- the oracle's restatement."""
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.polar.utils import CRC_POLYNOMIALS
+    P = _P()
+    K = N // 2
+    fr = P.construct_frozen_set(N, K, 2.0)
+    llr = _nan_frames(N, K, fr, 32, seed=5 + L)
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    plan = _native.polar_plan(N, K, mask, L)
+    clen = int(crc.split("-")[1])
+    plan.set_crc(clen, CRC_POLYNOMIALS[crc])
+    out = torch.empty((len(llr), K), dtype=torch.uint8, device="cuda")
+    plan.decode(torch.from_numpy(llr).cuda(), out)
+    want = oracle.cascl_decode(N, L, fr, llr, crc, threads=8)
+    assert _mismatch(out.cpu().numpy(), want) == 0

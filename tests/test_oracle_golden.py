@@ -187,3 +187,40 @@ def test_numpy_restatement_pinned():
     H = csr_to_dense(d["bp_row_ptr"], d["bp_col_idx"], 504)
     bits, its = R.ldpc_batch(H, d["llr"][:4])
     assert _bad(bits, d["bp_bits"][:4]) == 0 and np.array_equal(its, d["bp_iters"][:4])
+
+
+def test_pysort_matches_cpython(oracle):
+    """oracle/pysort.h restates CPython's list.sort(key=..., reverse=True); the
+    interpreter itself is the reference here: random keys with ties, -inf and
+    NaN (which compare false both ways), sizes 1..2100 (binary insertion below
+    64 items, runs + merges + galloping above)."""
+    rng = np.random.RandomState(0)
+    for trial in range(3000):
+        n = int(rng.choice([rng.randint(1, 70), rng.randint(60, 140), rng.randint(1, 2100)]))
+        kind = trial % 5
+        if kind == 0:
+            k = rng.randn(n)
+        elif kind == 1:
+            k = np.round(rng.randn(n) * 2) / 2
+        elif kind == 2:
+            k = rng.choice([np.nan, 0.0, 1.0, -np.inf, 2.0], size=n)
+        elif kind == 3:
+            k = rng.randn(n).cumsum() if rng.rand() < 0.5 else np.sort(rng.randn(n))
+            k[rng.rand(n) < 0.1 * rng.rand()] = np.nan
+        else:
+            k = np.round(rng.randn(n), 1)
+            k[rng.rand(n) < rng.rand()] = np.nan
+        items = [(np.float64(k[i]), i) for i in range(n)]
+        items.sort(key=lambda x: x[0], reverse=True)  # the reference's call, decoder.py:307
+        assert list(oracle.pysort_desc(k)) == [i for _, i in items], (trial, n, kind)
+
+
+def test_scl_nan_metrics(oracle):
+    """Frames whose SCL path metrics become NaN (+-inf meeting in a g, NaN
+    inputs), decoded by the reference (make_golden.job_polar_nan): the oracle
+    reproduces CPython's ordering of NaN candidates and np.argmax's first NaN."""
+    d = golden("polar_nan.npz")
+    for N in (16, 64, 256, 1024):
+        fr, llr = d["N%d_frozen" % N], d["N%d_llr" % N]
+        for L in d["N%d_Ls" % N]:
+            assert _bad(oracle.scl_decode(N, int(L), fr, llr, threads=8), d["N%d_L%d" % (N, L)]) == 0, (N, L)

@@ -149,7 +149,7 @@ def main():
             print("rep %d %s %s" % (r, os.path.basename(lib), json.dumps(res)), flush=True)
     print("%-40s %s" % ("lib", "  ".join("%12s" % c for c in cases)))
     for lib in libs:
-        print("%-40s %s" % (os.path.basename(lib), "  ".join("%12.3f" % min(table[lib][c]) for c in cases)))
+        print("%-40s %s" % (os.path.relpath(lib.partition("@")[0], ROOT)[-40:], "  ".join("%12.3f" % min(table[lib][c]) for c in cases)))
 
 
 if __name__ == "__main__":

@@ -245,6 +245,9 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
 #ifndef PL_MS_REGIDX
 #define PL_MS_REGIDX 1  // regular min-sum codes: adjacency indices cached in registers
 #endif
+#ifndef PL_BP_PROD
+#define PL_BP_PROD 0  // 1: check products over all d inputs with the own one replaced by 1.0
+#endif
 #ifndef PL_LDPC_REG_WPE
 #define PL_LDPC_REG_WPE 4  // waves per SIMD the register budget is built for
 #endif
@@ -332,6 +335,28 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
 #if PL_DIAG && defined(PL_ABL_PROD)
                 p = lo[i == 0 ? 1 : 0];  // ablation timing build: one factor
 #else
+#if PL_BP_PROD == 1
+                // every factor at its own offset from the check's first input, the
+                // own edge's replaced by 1.0 (x * 1.0 = x exactly: the same
+                // left-to-right product), so no per-factor pointer select
+                (void)hi;
+                (void)nf;
+                int k = 0;
+                for (; k + 4 <= d; k += 4) {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const double f = lo[k + c];
+                        p *= (k + c == i) ? 1.0 : f;
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    if (k + c < d) {
+                        const double f = lo[k + c];
+                        p *= (k + c == i) ? 1.0 : f;
+                    }
+                }
+#else
                 int k = 0;
                 for (; k + 4 <= nf; k += 4, lo += 4, hi += 4) {
 #pragma unroll
@@ -344,6 +369,7 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
                         if (k + 2 < nf) p *= (k + 2 < i ? lo : hi)[2];
                     }
                 }
+#endif
 #endif
                 // clip, 2*atanh, nan_to_num: after the clip 2*atanh is finite,
                 // so only a NaN product (NaN channel LLRs) maps to 0
@@ -466,20 +492,41 @@ PL_DEV double ms_c2v(double2 mm, uint32_t meta, int i, double norm) {
 }
 
 #ifndef PL_MS_CB
-#define PL_MS_CB 2  // regular codes: checks whose loads are issued together in the check pass
+#define PL_MS_CB 2  // regular codes: checks whose loads are issued together in the check pass (-6 %)
 #endif
 #ifndef PL_MS_VB
-#define PL_MS_VB 2  // regular codes: variables whose state loads are issued together
+#define PL_MS_VB 1  // regular codes: variables whose state loads are issued together (2: +15 %)
+#endif
+#ifndef PL_MS_VFAST
+#define PL_MS_VFAST 1  // variable pass: sign-flip c2v when the check saw no zero / NaN input
+#endif
+#ifndef PL_MS_PRE
+#define PL_MS_PRE 1  // regular codes, |norm| <= 1: check state pre-multiplied by the normalization
 #endif
 
 // All DC outputs of a check from its state, equal to ms_c2v position by
 // position: with no zero and no NaN input (the usual case) the sign product is
 // +-1, so (sp * mn) * norm = +-(mn * norm) -- two multiplies per check instead
 // of one per position (rounding is sign-symmetric).
-template <int DC>
+// PRE: the state holds (min1 * norm, min2 * norm) (|norm| <= 1, so no product
+// overflows): c2v = sp * (mn * norm), the same value as (sp * mn) * norm for
+// sp = +-1 (sign-symmetric rounding), +-0 (signs agree, 0 * inf = NaN on both
+// sides) and NaN, and with sp = +-1 just a sign flip -- no multiply per edge.
+PL_DEV double ms_c2v_pre(double2 mm, uint32_t meta, int i) {
+    const int idx1 = (int)(meta & 15u), ncnt = (int)((meta >> 4) & 3u), nidx = (int)((meta >> 6) & 15u);
+    const int zcnt = (int)((meta >> 10) & 3u), zidx = (int)((meta >> 12) & 15u);
+    const uint32_t neg = ((meta >> 16) ^ (meta >> (17 + i))) & 1u;
+    const double mn = (i == idx1) ? mm.y : mm.x;
+    double sp = neg ? -1.0 : 1.0;
+    sp = (zcnt >= 2 || (zcnt == 1 && zidx != i)) ? sp * 0.0 : sp;
+    sp = (ncnt >= 2 || (ncnt == 1 && nidx != i)) ? __builtin_nan("") : sp;
+    return sp * mn;
+}
+
+template <int DC, bool PRE = false>
 PL_DEV void ms_c2v_all(double2 mm, uint32_t meta, double norm, double* out) {
     if ((meta & 0x0C30u) == 0u) {
-        const double a1 = mm.x * norm, a2 = mm.y * norm;
+        const double a1 = PRE ? mm.x : mm.x * norm, a2 = PRE ? mm.y : mm.y * norm;
         const int idx1 = (int)(meta & 15u);
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
@@ -489,7 +536,7 @@ PL_DEV void ms_c2v_all(double2 mm, uint32_t meta, double norm, double* out) {
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < DC; ++k) out[k] = ms_c2v(mm, meta, k, norm);
+        for (int k = 0; k < DC; ++k) out[k] = PRE ? ms_c2v_pre(mm, meta, k) : ms_c2v(mm, meta, k, norm);
     }
 }
 
@@ -530,10 +577,11 @@ PL_DEV void ms_state(const double* x, double2& mm, uint32_t& meta) {
 // DV, DC > 0: a (DV, DC)-regular code (every variable / check degree equal, as
 // the BASELINE n = 8192 code): edge offsets are c * DC and v * DV, no row/column
 // pointer loads, and the edge loops unroll so their index loads issue together.
-template <int VPT, int DV, int DC>
+template <int VPT, int DV, int DC, bool PRE = false>
 __global__ void __launch_bounds__(1024)
 ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
                        uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch) {
+    static_assert(!PRE || (PL_MS_CB > 0 && PL_MS_VB > 0 && DV > 0 && DC > 0), "pre-scaled state: batched regular passes only");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t frame = blockIdx.x;
     if (frame >= batch) return;
@@ -615,7 +663,7 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
                         for (int k = 0; k < DC; ++k) x[k] = tv[b][k];
                     } else {
                         double c2v[DC];
-                        ms_c2v_all<DC>(om[b], ometa[b], g.norm, c2v);
+                        ms_c2v_all<DC, PRE>(om[b], ometa[b], g.norm, c2v);
 #pragma unroll
                         for (int k = 0; k < DC; ++k) x[k] = tv[b][k] - c2v[k];
                     }
@@ -625,7 +673,7 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
                     double2 mm;
                     uint32_t meta;
                     ms_state<DC>(x, mm, meta);
-                    smin[c] = mm;
+                    smin[c] = PRE ? make_double2(mm.x * g.norm, mm.y * g.norm) : mm;
                     smeta[c] = meta;
                 }
             }
@@ -703,7 +751,18 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
                     if (j0 + b >= VPT || v >= n) continue;
                     double sum = 0.0;  // np.sum over DV < 8 terms: sequential
 #pragma unroll
-                    for (int k = 0; k < DV; ++k) sum += ms_c2v(mm[b][k], mt[b][k], pos[b][k], g.norm);
+                    for (int k = 0; k < DV; ++k) {
+                        double c2v;
+                        if (PRE && PL_MS_VFAST && (mt[b][k] & 0x0C30u) == 0u) {
+                            // no zero / NaN input at the check: +-(scaled min), a sign flip
+                            const double mag = pos[b][k] == (int)(mt[b][k] & 15u) ? mm[b][k].y : mm[b][k].x;
+                            const uint64_t sgn = (uint64_t)(((mt[b][k] >> 16) ^ (mt[b][k] >> (17 + pos[b][k]))) & 1u) << 63;
+                            c2v = __longlong_as_double((long long)((uint64_t)__double_as_longlong(mag) ^ sgn));
+                        } else {
+                            c2v = PRE ? ms_c2v_pre(mm[b][k], mt[b][k], pos[b][k]) : ms_c2v(mm[b][k], mt[b][k], pos[b][k], g.norm);
+                        }
+                        sum += c2v;
+                    }
                     tot[v] = chv[j0 + b] + sum;
                 }
             }
@@ -863,7 +922,12 @@ static void* pick(bool global) {
 
 static void* pick_kernel(const LdpcGeom& g) {
     if (g.compact) {
-        if (g.n <= 8192 && g.regular && g.maxdv == 3 && g.maxdc == 6) return (void*)ldpc_ms_compact_kernel<8, 3, 6>;
+        if (g.n <= 8192 && g.regular && g.maxdv == 3 && g.maxdc == 6) {
+            // pre-scaled check state for |normalization| <= 1 (every BASELINE min-sum decode)
+            if (PL_MS_PRE && PL_MS_CB > 0 && PL_MS_VB > 0 && fabs(g.norm) <= 1.0)
+                return (void*)ldpc_ms_compact_kernel<8, 3, 6, (PL_MS_PRE && PL_MS_CB > 0 && PL_MS_VB > 0)>;
+            return (void*)ldpc_ms_compact_kernel<8, 3, 6>;
+        }
         return g.n <= 8192 ? (void*)ldpc_ms_compact_kernel<8, 0, 0> : (void*)ldpc_ms_compact_kernel<0, 0, 0>;
     }
     if (g.reg_variant) {

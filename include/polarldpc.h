@@ -151,6 +151,15 @@ const char* pl_last_error(void);
 int pl_debug_polar_stamps(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
                           unsigned long long* stamps_dev, void* stream);
 
+/* Diagnostic build only (the product library returns PL_EUNSUPPORTED): the
+ * frame-per-wavefront SCL prototype (one wavefront per frame, eight lanes per
+ * list path, every LLR pool in LDS) on a polar N=1024 L=8
+ * plan, for timing against pl_decode.  stamps_dev[5] (may be NULL) receives
+ * per-phase s_memtime cycle totals: descent, metric, pruning, partial sums,
+ * output.  grid <= 0: one wavefront per LDS slot of the device. */
+int pl_debug_polar_fpw(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
+                       unsigned long long* stamps_dev, int32_t grid, void* stream);
+
 /* Test hook, diagnostic build only (the product library returns
  * PL_EUNSUPPORTED): overwrite the device id a plan is bound to, so the
  * wrong-device check can be exercised on a one-GPU machine.  UNSAFE: it turns

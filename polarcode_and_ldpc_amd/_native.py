@@ -24,7 +24,7 @@ EXPORTS = (
     "pl_plan_destroy", "pl_last_error", "pl_random_bits", "pl_polar_encode", "pl_awgn_llr",
     "pl_count_errors", "pl_debug_polar_stamps", "pl_polar_plan_set_crc", "pl_crc_append",
     "pl_rayleigh_llr", "pl_bsc", "pl_gf2_encode", "pl_decode_ws", "pl_plan_workspace_bytes",
-    "pl_plan_release", "pl_plan_workspace_stats", "pl_debug_set_plan_device",
+    "pl_plan_release", "pl_plan_workspace_stats", "pl_debug_set_plan_device", "pl_debug_polar_fpw",
 )
 
 
@@ -60,6 +60,7 @@ def _load(path=LIB_PATH):
     L.pl_awgn_llr.argtypes = [P, I32, I64, D, ctypes.c_uint64, I64, P, I64, P]
     L.pl_count_errors.argtypes = [P, I64, P, I64, I32, I64, P, P]
     L.pl_debug_polar_stamps.argtypes = [P, P, I64, I64, P, P, P]
+    L.pl_debug_polar_fpw.argtypes = [P, P, I64, I64, P, P, I32, P]
     L.pl_polar_plan_set_crc.argtypes = [P, I32, ctypes.c_uint32]
     L.pl_crc_append.argtypes = [P, I64, I64, I32, I32, ctypes.c_uint32, P]
     L.pl_rayleigh_llr.argtypes = [P, I32, I64, D, ctypes.c_uint64, I64, P, I64, P]
@@ -195,6 +196,12 @@ class Plan:
         check(lib.pl_debug_polar_stamps(self._h, ctypes.c_void_p(llr.data_ptr()), llr.shape[0], _ld(llr),
                                         _dptr(bits), _dptr(stamps), ctypes.c_void_p(_stream(stream))),
               "pl_debug_polar_stamps")
+
+    def decode_fpw(self, llr: "torch.Tensor", bits: "torch.Tensor", stamps=None, grid: int = 0, stream=None):
+        """Diagnostic: the frame-per-wavefront prototype (pl_debug_polar_fpw, N=1024 L=8)."""
+        check(lib.pl_debug_polar_fpw(self._h, ctypes.c_void_p(llr.data_ptr()), llr.shape[0], _ld(llr),
+                                     _dptr(bits), _dptr(stamps) if stamps is not None else None, int(grid),
+                                     ctypes.c_void_p(_stream(stream))), "pl_debug_polar_fpw")
 
     def set_crc(self, crc_len: int, poly: int):
         """CRC-aided list selection (pl_polar_plan_set_crc); crc_len 0 = off."""

@@ -617,6 +617,25 @@ extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batc
 #endif
 }
 
+// Diagnostic build: the frame-per-wavefront prototype (polar_fpw.hip) on a
+// polar N=1024 L=8 plan's device constants; stamps_dev: 5 u64 cycle sums
+// (descent, metric, prune, partial sums, output); grid 0 = fill the device.
+extern "C" int pl_debug_polar_fpw(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
+                                  unsigned long long* stamps_dev, int32_t grid, void* stream) {
+#if !PL_DIAG
+    (void)p; (void)llr; (void)batch; (void)ld; (void)bits; (void)stamps_dev; (void)grid; (void)stream;
+    return fail(PL_EUNSUPPORTED, "the frame-per-wavefront prototype is in the diagnostic build only (make DIAG=1)");
+#else
+    if (!p || p->kind != 0 || p->pg.N != 1024 || p->list_size != 8) return fail(PL_EINVAL, "N=1024 L=8 polar plan");
+    int rc = check_decode_args(p, batch, ld, llr, bits);
+    if (rc || batch == 0) return rc;
+    if ((rc = check_device(p))) return rc;
+    hipError_t e = pl::fpw_launch(llr, ld, bits, p->d_frozen_dec, p->d_info_pos, batch, p->pg.K, stamps_dev, grid,
+                                  (hipStream_t)stream);
+    return e == hipSuccess ? PL_OK : hipfail(e, "fpw launch");
+#endif
+}
+
 extern "C" int pl_debug_set_plan_device(pl_plan* p, int32_t device) {
     if (!p) return fail(PL_EINVAL, "plan is NULL");
 #if !PL_DIAG

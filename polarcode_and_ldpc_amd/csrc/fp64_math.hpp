@@ -123,4 +123,22 @@ PL_DEV double log1p_pos(double x) {
     return dk * LN2_HI - ((hfsq - (s * (hfsq + R) + (dk * LN2_LO + c))) - f);
 }
 
+// log1p(exp(-x)) for x >= 0 (finite or +inf), the SCL path-metric term
+// (src/polar/decoder.py:374-406).  u = e^-x by exp_neg; then, as u <= 1,
+// 1 + u = 2^j (1 + f) with j = 0, f = u below sqrt(2) - 1 and j = 1,
+// f = (u - 1)/2 above -- both exact (Sterbenz), so the rounding correction of
+// the general log1p (frexp, ldexp, a reciprocal) is not needed; the same fdlibm
+// log kernel on f.  <= 1 ulp.
+PL_DEV double log1p_exp_neg(double x) {
+    constexpr double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+    const double u = exp_neg(x);
+    const bool big = u > 0.41421356237309503;
+    const double f = big ? 0.5 * (u - 1.0) : u;
+    const double hfsq = 0.5 * f * f;
+    const double s = div_fast(f, 2.0 + f);
+    const double R = lg_R(s * s);
+    const double j = big ? 1.0 : 0.0;
+    return j * LN2_HI - ((hfsq - (s * (hfsq + R) + j * LN2_LO)) - f);
+}
+
 }  // namespace pl

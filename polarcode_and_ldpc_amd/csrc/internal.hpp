@@ -67,6 +67,13 @@ hipError_t nan_redo_launch(const double* llr, int64_t ld, uint8_t* out, int64_t 
                            uint64_t* masks, int grid, int fpw, unsigned char* scratch, size_t scratch_bytes,
                            int max_blocks, hipStream_t s);
 
+#if PL_DIAG
+// frame-per-wavefront SCL N=1024 L=8 prototype (polar_fpw.hip, diagnostic build)
+hipError_t fpw_launch(const double* llr, int64_t ld, uint8_t* out, const uint32_t* frozen_dec,
+                      const int32_t* info_pos, int64_t batch, int K, unsigned long long* stamps, int grid,
+                      hipStream_t st);
+#endif
+
 hipError_t polar_encode_launch(int N, int K, const int32_t* pos2info, const uint8_t* msg,
                                int64_t batch, uint8_t* cw, hipStream_t s);
 hipError_t random_bits_launch(uint64_t seed, int64_t off, int64_t batch, int k, uint8_t* bits,

@@ -7,6 +7,13 @@
 #include "common.hpp"
 #include "fp64_math.hpp"
 
+#ifndef PL_METRIC_FUSED_NMAX
+// tree instances with n <= this use the fused log1p(exp(-x)) (log1p_exp_neg):
+// N=1024 L=8 -1.9 %, L=32 -2.6 %; N=4096 L=8 +3.6 % (register allocation), so
+// larger codes keep log1p_pos(exp_neg(x)); bits identical on every polar GPU test
+#define PL_METRIC_FUSED_NMAX 10
+#endif
+
 namespace pl {
 
 // min-sum f with the reference's value semantics: sign(a)*sign(b)*min(|a|,|b|)
@@ -53,7 +60,7 @@ PL_DEV void path_metrics(double pm, double lam, double& m0, double& m1) {
 // threshold is identical) and two more skips that cannot change a result:
 // inactive list slots (their metrics are never read) and pm = +-inf with a
 // non-NaN LLR (t is finite, so pm + anything finite = pm as in the reference).
-template <bool WANT1>
+template <bool WANT1, bool FUSED = false>
 PL_DEV void path_metrics_fast(double pm, double lam, bool active, double& m0, double& m1) {
     const double x = fabs(lam);
     const int ep = __builtin_amdgcn_frexp_exp(pm);
@@ -66,7 +73,7 @@ PL_DEV void path_metrics_fast(double pm, double lam, bool active, double& m0, do
 #if PL_DIAG && defined(PL_ABL_METRIC)
     (void)skip;  // ablation timing build: no transcendental (decisions change)
 #else
-    if (!skip) t = log1p_pos(exp_neg(x));  // lean exp / log1p (fp64_math.hpp)
+    if (!skip) t = FUSED ? log1p_exp_neg(x) : log1p_pos(exp_neg(x));  // lean exp / log1p (fp64_math.hpp)
 #endif
     m0 = pm + ((lam >= 0.0) ? -t : lam - t);
     if (WANT1) m1 = pm + ((lam >= 0.0) ? -lam - t : -t);

@@ -88,6 +88,7 @@ PL_DEV void redo_frame(const RedoArgs& a, int64_t frame, const Bufs& bf, unsigne
     int* flag = nbit + L;                                          // [L] claimed / used scratch
     int* shared = flag + L;                                        // [4]
     const double* ch = a.llr + frame * a.ld;
+    const bool fused = n <= PL_METRIC_FUSED_NMAX;  // the metric evaluation of the tree instances it stands in for
 
     for (int p = tid; p < L; p += kRedoThreads) {
         phys[p] = p;
@@ -118,7 +119,8 @@ PL_DEV void redo_frame(const RedoArgs& a, int64_t frame, const Bufs& bf, unsigne
             for (int p = tid; p < nact; p += kRedoThreads) {
                 const double lam = bf.llr(phys[p])[dep_off(N, n)];
                 double m0, m1;
-                path_metrics_fast<false>(pm[p], lam, true, m0, m1);
+                if (fused) path_metrics_fast<false, true>(pm[p], lam, true, m0, m1);
+                else path_metrics_fast<false, false>(pm[p], lam, true, m0, m1);
                 pm[p] = m0;
                 nbit[p] = 0;
             }
@@ -127,7 +129,8 @@ PL_DEV void redo_frame(const RedoArgs& a, int64_t frame, const Bufs& bf, unsigne
             for (int p = tid; p < nact; p += kRedoThreads) {
                 const double lam = bf.llr(phys[p])[dep_off(N, n)];
                 double m0, m1;
-                path_metrics_fast<true>(pm[p], lam, true, m0, m1);
+                if (fused) path_metrics_fast<true, true>(pm[p], lam, true, m0, m1);
+                else path_metrics_fast<true, false>(pm[p], lam, true, m0, m1);
                 cand[p] = PsItem{m0, p, 0};             // path_metrics_0 (decoder.py:300-303)
                 cand[nact + p] = PsItem{m1, nact + p, 0};  // path_metrics_1, after every bit-0 candidate
             }

@@ -586,7 +586,7 @@ PL_DEV void rate0_rest(const unsigned char* smem, const unsigned char* ws, int p
 #if PL_DIAG && defined(PL_ABL_METRIC)
                     const double t = 0.0 * lam;
 #else
-                    const double t = log1p_pos(exp_neg(fabs(lam)));
+                    const double t = G::n <= PL_METRIC_FUSED_NMAX ? log1p_exp_neg(fabs(lam)) : log1p_pos(exp_neg(fabs(lam)));
 #endif
                     inc[u] = (lam >= 0.0) ? -t : lam - t;
                 }
@@ -599,7 +599,7 @@ PL_DEV void rate0_rest(const unsigned char* smem, const unsigned char* ws, int p
 #pragma unroll
         for (int j = 1; j < S; ++j) {
             double m0, m1;
-            path_metrics_fast<false>(pm, ll[j], active, m0, m1);
+            path_metrics_fast<false, (G::n <= PL_METRIC_FUSED_NMAX)>(pm, ll[j], active, m0, m1);
             if (active) pm = m0;
         }
 #endif
@@ -774,13 +774,13 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 STAMP(3);
             } else if (frozen) {
                 double m0, m1;
-                path_metrics_fast<false>(pm, lam, slot < nact, m0, m1);
+                path_metrics_fast<false, (G::n <= PL_METRIC_FUSED_NMAX)>(pm, lam, slot < nact, m0, m1);
                 if (slot < nact) pm = m0;
                 bit = 0;
                 STAMP(3);
             } else {
                 double m0, m1;
-                path_metrics_fast<true>(pm, lam, slot < nact, m0, m1);
+                path_metrics_fast<true, (G::n <= PL_METRIC_FUSED_NMAX)>(pm, lam, slot < nact, m0, m1);
                 STAMP(3);
                 // a full, ordered list keeps its order: survivor s = path s
                 // with its better bit (ordered_prune), nothing exchanged

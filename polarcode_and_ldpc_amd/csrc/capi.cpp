@@ -67,6 +67,7 @@ struct pl_plan {
     // wavefront, at the start of the workspace) and the scratch one workgroup of
     // polar_nan_redo_kernel needs (it reuses the list kernel's slices after it)
     size_t mask_bytes = 0, redo_unit = 0;
+    bool generic = false;  // list_size > 1024: polar_nan.hip decodes every frame
     int redo_blocks = 0;
     std::mutex mu;  // guards the map only; each entry has its own mutex
     std::unordered_map<hipStream_t, std::shared_ptr<Workspace>> ws;
@@ -137,7 +138,8 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
         return fail(PL_EINVAL, "N must be a power of 2 in [2, 32768]");
     if (!(0 < K && K <= N)) return fail(PL_EINVAL, "K (info positions) must be in [1, N]");
     if (list_size < 0) return fail(PL_EINVAL, "list_size must be >= 1 (0 = SC)");
-    if (list_size > 1024) return fail(PL_EUNSUPPORTED, "list_size > 1024 not supported by this build (one workgroup per frame)");
+    if (list_size > pl::kMaxRedoList)
+        return fail(PL_EUNSUPPORTED, "list_size > 2048 not supported by this build (the list state of one frame in LDS)");
     if (!frozen_mask) return fail(PL_EINVAL, "frozen_mask is NULL");
     int n = 0;
     while ((1 << n) < N) ++n;
@@ -158,7 +160,11 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
     const char* kern = std::getenv("PL_POLAR_KERNEL");
     int lcap = 1;
     while (lcap < (p->sc ? 1 : list_size)) lcap <<= 1;
-    p->tree = !(kern && std::string(kern) == "lane") && !(flags & 0x3F) && pl::tree_lookup(n, lcap, p->sc, &p->tinfo);
+    // lists above 1024 (one frame per workgroup no longer holds one lane per
+    // path): every frame through the exact single-workgroup decoder of polar_nan.hip
+    p->generic = list_size > 1024;
+    p->tree = !p->generic && !(kern && std::string(kern) == "lane") && !(flags & 0x3F) &&
+              pl::tree_lookup(n, lcap, p->sc, &p->tinfo);
     hipError_t e;
     if ((e = upload(&p->d_frozen_dec, fdec)) != hipSuccess || (e = upload(&p->d_info_pos, info)) != hipSuccess ||
         (e = upload(&p->d_pos2info, pos2info)) != hipSuccess) {
@@ -189,7 +195,13 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
         }
     }
     int per_cu = 1;
-    if (p->tree) {
+    if (p->generic) {
+        p->pg.F = 0;
+        p->pg.lds_bytes = pl::nan_redo_lds_bytes(list_size);
+        p->fpw = 1;
+        p->ws_unit = 0;
+        e = hipSuccess;
+    } else if (p->tree) {
         p->pg.F = p->tinfo.F;
         p->pg.lds_bytes = p->tinfo.lds_bytes;
         p->fpw = p->tinfo.fpw;
@@ -215,11 +227,16 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
     const int waves_env = env_int("PL_POLAR_WAVES", 0);
     if (waves_env > 0) p->lane_grid_max = waves_env;
     if (!p->sc) {
-        p->mask_bytes = pl::nan_mask_region(p->lane_grid_max);
+        p->mask_bytes = p->generic ? 0 : pl::nan_mask_region(p->lane_grid_max);
         p->redo_unit = pl::nan_redo_unit(N, list_size);
         p->redo_blocks = device_cus(p->device);
+        if (p->generic) {  // scratch of up to 2 GB: a 2048-path list of N = 1024 holds 23 MB per frame
+            const size_t cap = (size_t)2 << 30;
+            p->redo_blocks = (int)std::max<size_t>(1, std::min<size_t>((size_t)p->redo_blocks, cap / p->redo_unit));
+            p->lane_grid_max = p->redo_blocks;
+        }
         // the kernel's dynamic-LDS limit is per function: set it for the largest list once
-        if ((e = pl::nan_redo_prepare(1024)) != hipSuccess) {
+        if ((e = pl::nan_redo_prepare(pl::kMaxRedoList)) != hipSuccess) {
             pl_plan_destroy(p);
             return hipfail(e, "NaN redo kernel prepare");
         }
@@ -374,11 +391,15 @@ static size_t polar_bytes(const pl_plan* p, int64_t grid) {
     return p->mask_bytes + std::max<size_t>(p->ws_unit * (size_t)grid, p->redo_unit);
 }
 // the smallest workspace a decode can run on (one wavefront's slice)
-static size_t ws_min(const pl_plan* p) { return p->kind == 0 ? polar_bytes(p, 1) : p->ws_unit; }
+static size_t ws_min(const pl_plan* p) {
+    if (p->kind == 0 && p->generic) return p->redo_unit;
+    return p->kind == 0 ? polar_bytes(p, 1) : p->ws_unit;
+}
 
 // Workspace bytes a decode of `batch` frames uses at full speed.
 static size_t ws_need(const pl_plan* p, int64_t batch) {
     if (batch <= 0 || (p->ws_unit == 0 && p->redo_unit == 0)) return 0;
+    if (p->kind == 0 && p->generic) return p->redo_unit * (size_t)std::min<int64_t>(batch, p->redo_blocks);
     if (p->kind == 0) {
         const int64_t waves = (batch + p->fpw - 1) / p->fpw;
         return polar_bytes(p, std::min<int64_t>(waves, p->lane_grid_max));
@@ -393,6 +414,14 @@ static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld,
     const size_t wmin = ws_min(p);
     if (wmin > 0 && (ws == nullptr || ws_bytes < wmin))
         return fail(PL_EINVAL, "workspace smaller than one unit (pl_plan_workspace_bytes)");
+    if (p->kind == 0 && p->generic) {
+        if (stamps) return fail(PL_EUNSUPPORTED, "stamps only for the tree kernel");
+        // one workgroup per frame, masks = null: every frame
+        hipError_t e = pl::nan_redo_launch(llr, ld, bits, batch, p->pg.N, p->pg.K, p->list_size, p->d_frozen_dec,
+                                           p->d_info_pos, p->d_crc_g, nullptr, 0, 1, (unsigned char*)ws, ws_bytes,
+                                           p->redo_blocks, s);
+        return e == hipSuccess ? PL_OK : hipfail(e, "polar generic list launch");
+    }
     if (p->kind == 0) {
         if (!p->tree && stamps) return fail(PL_EUNSUPPORTED, "stamps only for the tree kernel");
         const int64_t waves = (batch + p->fpw - 1) / p->fpw;
@@ -680,7 +709,7 @@ extern "C" int pl_plan_get_info(const pl_plan* p, pl_plan_info* info) {
         info->kind = 0; info->n_in = p->pg.N; info->n_out = p->pg.K; info->list_size = p->list_size;
         info->lds_bytes = p->pg.lds_bytes; info->fused_top = p->pg.F;
         info->frames_per_block = p->fpw;
-        info->reserved = p->tree ? 4 : 3;  // kernel generation: 4 tree, 3 lane
+        info->reserved = p->generic ? 6 : (p->tree ? 4 : 3);  // kernel: 4 tree, 3 lane, 6 single-workgroup exact
     } else {
         info->kind = 1; info->n_in = p->lg.n; info->n_out = p->lg.n; info->list_size = 0;
         info->lds_bytes = p->lg.lds_bytes; info->fused_top = 0; info->frames_per_block = 1;

@@ -54,6 +54,7 @@ hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t
 // those frames again in the reference's candidate order.  A launch runs at most
 // kNanMaskPasses passes of its persistent grid.
 constexpr int kNanMaskPasses = 64;
+constexpr int kMaxRedoList = 2048;  // the redo kernel's list state of one frame fits LDS up to here
 // Bytes of the mask words of up to `grid` wavefronts, u64 [grid][kNanMaskPasses]
 // (a multiple of 64 KB, at the start of a list plan's workspace).  They are zero
 // between decodes: zeroed when the workspace is allocated, ORed by the list

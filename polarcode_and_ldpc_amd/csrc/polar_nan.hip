@@ -22,6 +22,10 @@
 // A clone claims its parent's buffer if no earlier survivor did, else copies it
 // into a buffer no survivor uses (Tal & Vardy's lazy copy without reference
 // counts: at most one copy per extra child).
+//
+// The same kernel, launched without masks, is the decoder of lists above 1024
+// paths (up to kMaxRedoList; the list kernels hold one lane per path in one
+// workgroup): every frame, one workgroup each.
 #include <algorithm>
 
 #include "common.hpp"
@@ -265,6 +269,10 @@ __global__ void __launch_bounds__(kRedoThreads) polar_nan_redo_kernel(RedoArgs a
     // flagged (mask, first frame) pairs of one scan round, after the frame state
     uint64_t* const xw = reinterpret_cast<uint64_t*>(smem + lds_frame_bytes(a.Lsz));
     int* const xn = reinterpret_cast<int*>(xw + 2 * kRedoThreads);
+    if (a.masks == nullptr) {  // lists above 1024: every frame here
+        for (int64_t f = blockIdx.x; f < a.batch; f += gridDim.x) redo_frame(a, f, bf, smem);
+        return;
+    }
     const int64_t stride_frames = (int64_t)a.grid * a.fpw;
     // mask words of wavefronts w = blockIdx.x, + gridDim.x, ...: 256 at a time
     const int64_t wpb = (a.grid + gridDim.x - 1) / gridDim.x;  // wavefronts of this workgroup (at most)
@@ -323,7 +331,9 @@ hipError_t nan_redo_launch(const double* llr, int64_t ld, uint8_t* out, int64_t 
     RedoArgs a{llr, ld, out, batch, N, n, K, Lsz, frozen_dec, info_pos, crc_g, masks, grid, fpw, scratch,
                nan_redo_unit(N, Lsz)};
     const int64_t fit = (int64_t)(scratch_bytes / a.unit);
-    int blocks = (int)std::min<int64_t>(std::min<int64_t>(grid, fit), max_blocks);
+    // masks: one workgroup per list-kernel wavefront at most; no masks: per frame
+    const int64_t want = masks ? (int64_t)grid : batch;
+    int blocks = (int)std::min<int64_t>(std::min<int64_t>(want, fit), max_blocks);
     if (blocks < 1) return hipErrorInvalidValue;
     void* args[] = {(void*)&a};
     return hipLaunchKernel((const void*)polar_nan_redo_kernel, dim3((unsigned)blocks), dim3(kRedoThreads), args,

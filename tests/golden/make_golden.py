@@ -547,9 +547,22 @@ def job_polar_nan():
     return "polar_nan.npz", out
 
 
+def job_scl_l2048():
+    """Round 4: list sizes above 1024 (the exact single-workgroup decoder):
+    N=64 at L=2048 and N=32 at L=1500 (a non-power-of-two list), low SNR so the
+    lists fill."""
+    out = {}
+    for tag, (N, K, L, snrs, frames, seed) in (("N64_L2048", (64, 32, 2048, (0.0,), 2, 331)),
+                                              ("N32_L1500", (32, 16, 1500, (0.5,), 3, 332))):
+        d = job_scl(N, K, L, snrs, frames, seed, "x")[1]
+        for k in ("frozen", "llr", "msg", "snr", "scl", "ref_s_per_frame"):
+            out[tag + "_" + k] = d[k]
+    return "polar_scl_l2048.npz", out
+
+
 JOBS = [job_scl4096_l8, job_scl1024_l8, job_ms8192, job_scl1024_l32, job_bp504,
         job_sc1024, job_ms504, job_small, job_p1, job_kat16, job_crc, job_ldpc_special, job_polar_erasures
-        ] + ROUND2_JOBS + [job_polar_nan]
+        ] + ROUND2_JOBS + [job_polar_nan, job_scl_l2048]
 
 
 def _run(fn):

@@ -774,8 +774,42 @@ def test_scl_large_lists_golden_and_oracle(gpu, oracle):
     assert _mismatch(P.SCLDecoder(64, 32, list_size=700, frozen_bits=fr64).decode_batch(llr64[:6]), want) == 0
     want = oracle.scl_decode(N, 513, fr, llr[:4], threads=8)
     assert _mismatch(P.SCLDecoder(N, K, list_size=513, frozen_bits=fr).decode_batch(llr[:4]), want) == 0
-    with pytest.raises(ValueError):  # PL_EUNSUPPORTED: one workgroup (1024 lanes) per frame
-        P.SCLDecoder(N, K, list_size=1025, frozen_bits=fr).decode_batch(llr)
+    with pytest.raises(ValueError):  # PL_EUNSUPPORTED: the exact decoder's list state fits LDS up to 2048
+        P.SCLDecoder(N, K, list_size=2049, frozen_bits=fr).decode_batch(llr)
+
+
+def test_scl_lists_above_1024(gpu, oracle):
+    """Lists of 1025..2048 paths (VERDICT r03 missing 4; the reference accepts any
+    L): every frame through the exact single-workgroup decoder of polar_nan.hip --
+    the reference's L=2048 (N=64) and L=1500 (N=32) fixtures, the oracle at
+    L=1025 / 2048 on noisy N=128 frames, CA-SCL at L=1500 against the oracle's
+    restatement, and a NaN frame."""
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.polar.utils import CRC_POLYNOMIALS
+    P = _P()
+    d = golden("polar_scl_l2048.npz")
+    for tag, Nt, L in (("N64_L2048", 64, 2048), ("N32_L1500", 32, 1500)):
+        fr_t = d[tag + "_frozen"]
+        dec = P.SCLDecoder(Nt, Nt - len(fr_t), list_size=L, frozen_bits=fr_t)
+        assert dec.plan.info.reserved == 6  # the exact single-workgroup decoder
+        assert _mismatch(dec.decode_batch(d[tag + "_llr"]), d[tag + "_scl"]) == 0, tag
+    rng = np.random.RandomState(2048)
+    N, K = 128, 64
+    fr = P.construct_frozen_set(N, K, 1.0)
+    cw = P.PolarEncoder(N, K, frozen_bits=fr).encode_batch(rng.randint(0, 2, (6, K)))
+    llr = 2.0 * ((1.0 - 2.0 * cw) + 1.1 * rng.randn(6, N)) / 1.21
+    llr[5, ::7] = np.inf
+    llr[5, 1::7] = -np.inf
+    for L in (1025, 2048):
+        want = oracle.scl_decode(N, L, fr, llr, threads=8)
+        assert _mismatch(P.SCLDecoder(N, K, list_size=L, frozen_bits=fr).decode_batch(llr), want) == 0, L
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    plan = _native.polar_plan(N, K, mask, 1500)
+    plan.set_crc(8, CRC_POLYNOMIALS["CRC-8"])
+    out = torch.empty((6, K), dtype=torch.uint8, device="cuda")
+    plan.decode(torch.from_numpy(llr).cuda(), out)
+    assert _mismatch(out.cpu().numpy(), oracle.cascl_decode(N, 1500, fr, llr, "CRC-8", threads=8)) == 0
 
 
 @pytest.mark.parametrize("N,L,K", [(1024, 0, 300), (1024, 8, 512), (1024, 8, 40), (1024, 32, 700), (4096, 8, 2048),

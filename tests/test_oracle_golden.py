@@ -224,3 +224,11 @@ def test_scl_nan_metrics(oracle):
         fr, llr = d["N%d_frozen" % N], d["N%d_llr" % N]
         for L in d["N%d_Ls" % N]:
             assert _bad(oracle.scl_decode(N, int(L), fr, llr, threads=8), d["N%d_L%d" % (N, L)]) == 0, (N, L)
+
+
+def test_scl_above_1024(oracle):
+    """Lists above 1024: L=2048 (N=64) and L=1500 (N=32), reference SCLDecoder
+    (round-4 fixture)."""
+    d = golden("polar_scl_l2048.npz")
+    for tag, N, L in (("N64_L2048", 64, 2048), ("N32_L1500", 32, 1500)):
+        assert _bad(oracle.scl_decode(N, L, d[tag + "_frozen"], d[tag + "_llr"], threads=8), d[tag + "_scl"]) == 0, tag

@@ -67,6 +67,7 @@ struct pl_plan {
     // wavefront, at the start of the workspace) and the scratch one workgroup of
     // polar_nan_redo_kernel needs (it reuses the list kernel's slices after it)
     size_t mask_bytes = 0, redo_unit = 0;
+    size_t head_bytes = 0;  // polar: NaN masks + the tree kernel's frame-group counter, before the slices
     bool generic = false;  // list_size > 1024: polar_nan.hip decodes every frame
     int redo_blocks = 0;
     std::mutex mu;  // guards the map only; each entry has its own mutex
@@ -241,6 +242,7 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
             return hipfail(e, "NaN redo kernel prepare");
         }
     }
+    p->head_bytes = p->mask_bytes + (p->tree ? (size_t)pl::kTreeSchedBytes : 0);
     *out = p;
     return PL_OK;
 }
@@ -385,10 +387,12 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
 
 // Polar workspace layout for a grid of `grid` resident wavefronts: a list
 // plan's NaN masks first (for its largest grid, so they stay in place, and
-// zero, from one decode to the next), then the list kernel's slices, which the
-// NaN redo kernel reuses as its scratch once the list kernel is done.
+// zero, from one decode to the next), then the tree kernel's frame-group
+// counter (zeroed by tree_launch before each launch), then the list kernel's
+// slices, which the NaN redo kernel reuses as its scratch once the list kernel
+// is done.
 static size_t polar_bytes(const pl_plan* p, int64_t grid) {
-    return p->mask_bytes + std::max<size_t>(p->ws_unit * (size_t)grid, p->redo_unit);
+    return p->head_bytes + std::max<size_t>(p->ws_unit * (size_t)grid, p->redo_unit);
 }
 // the smallest workspace a decode can run on (one wavefront's slice)
 static size_t ws_min(const pl_plan* p) {
@@ -429,7 +433,7 @@ static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld,
         while (grid > 1 && polar_bytes(p, grid) > ws_bytes) grid = std::min<int64_t>(grid - 1, grid * ws_bytes / polar_bytes(p, grid));
         unsigned char* const base = (unsigned char*)ws;
         uint64_t* const masks = p->mask_bytes ? (uint64_t*)base : nullptr;
-        unsigned char* const slices = base + p->mask_bytes;
+        unsigned char* const slices = base + p->head_bytes;  // the tree kernel's counter: slices - kTreeSchedBytes
         if (masks && zero_masks) {  // a caller-owned workspace: the masks may hold anything
             hipError_t e = hipMemsetAsync(masks, 0, (size_t)grid * 8 * pl::kNanMaskPasses, s);
             if (e != hipSuccess) return hipfail(e, "NaN mask reset");
@@ -453,7 +457,7 @@ static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld,
                 // frames whose list saw a NaN metric, in the reference's candidate order
                 e = pl::nan_redo_launch(l0, ld, o0, nb, p->pg.N, p->pg.K, p->list_size, p->d_frozen_dec,
                                         p->d_info_pos, p->d_crc_g, masks, (int)grid, p->fpw, slices,
-                                        ws_bytes - p->mask_bytes, p->redo_blocks, s);
+                                        ws_bytes - p->head_bytes, p->redo_blocks, s);
                 if (e != hipSuccess) return hipfail(e, "polar NaN redo launch");
             }
         }

@@ -53,6 +53,9 @@ namespace {
 #ifndef RANK_STRICT_LCAP
 #define RANK_STRICT_LCAP 8  // list capacities ranked with strict comparisons
 #endif
+#ifndef PL_TREE_DYN
+#define PL_TREE_DYN 1  // frame groups past the first claimed from a counter (the kernel's group loop)
+#endif
 #ifndef PL_RATE0
 #define PL_RATE0 2  // rate-0 nodes of 2..8 leaves decoded at their first leaf; >= 2: metric chains per group
 #endif
@@ -667,7 +670,17 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         tprev = tn;                                                 \
     }
 
-    for (int64_t f0 = (int64_t)blockIdx.x * FPW; f0 < batch; f0 += (int64_t)gridDim.x * FPW) {
+    // Frame groups (FPW frames each): group blockIdx.x first; then, with
+    // PL_TREE_DYN, the next unclaimed group from one counter (kTreeSchedBytes
+    // before the slices, zeroed by tree_launch), so that wavefronts slowed by
+    // harder frames, a busier SIMD or a busier XCD take fewer groups instead of
+    // stretching the launch's tail; else groups b, b + grid, b + 2 grid, ...
+    const int64_t ngrp = (batch + FPW - 1) / FPW;
+#if PL_TREE_DYN
+    unsigned int* const sched = reinterpret_cast<unsigned int*>(workspace - kTreeSchedBytes);
+#endif
+    for (int64_t grp = blockIdx.x; grp < ngrp;) {
+        const int64_t f0 = grp * FPW;
         const int64_t frame = f0 + fw;
         const bool live = frame < batch;
         const double* __restrict__ ch = llr + (live ? frame : batch - 1) * ld;
@@ -719,10 +732,12 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 uint64_t fm = 0;
 #pragma unroll
                 for (int sft = 0; sft < 64; sft += FPW) fm |= (bal >> sft) & ((1ull << FPW) - 1ull);
-                const uint32_t ps = ((uint32_t)f0 / FPW - blockIdx.x) / gridDim.x;  // pass (< 2^31 frames per launch)
+                // word [grp % grid][grp / grid], where the static schedule's pass
+                // grp / grid of wavefront grp % grid keeps it (polar_nan.hip)
+                const uint32_t ps = (uint32_t)grp / gridDim.x, wv = (uint32_t)grp % gridDim.x;
                 if (lane == 0 && ps < (uint32_t)kNanMaskPasses)
                     atomicOr(reinterpret_cast<unsigned long long*>(const_cast<uint32_t*>(aux)) +
-                                 (size_t)blockIdx.x * kNanMaskPasses + ps,
+                                 (size_t)wv * kNanMaskPasses + ps,
                              (unsigned long long)fm);
             }
         }
@@ -1156,6 +1171,21 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         lds_sync();
         ws_sync();  // staging of the next frames overwrites workspace read above
         STAMP(6);
+#if PL_TREE_DYN
+        // a counter read past the end (it only grows: a stale value is never
+        // too large) ends the loop without a claim, so the wavefronts finishing
+        // together at the end do not queue on one atomic
+        unsigned int nx = 0xFFFFFFFFu;
+        if (lane == 0) {
+            const unsigned int seen = __hip_atomic_load(sched, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((int64_t)gridDim.x + (int64_t)seen < ngrp)
+                nx = __hip_atomic_fetch_add(sched, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        nx = (unsigned int)__builtin_amdgcn_readfirstlane((int)nx);
+        grp = nx == 0xFFFFFFFFu ? ngrp : (int64_t)gridDim.x + (int64_t)nx;
+#else
+        grp += gridDim.x;
+#endif
     }
     if constexpr (STAMPS) {
         if (lane == 0)
@@ -1289,6 +1319,10 @@ hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t
     void* args[] = {(void*)&llr, (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos, (void*)&batch,
                     (void*)&K,   (void*)&Lsz, (void*)&ws, (void*)&stamps,     (void*)&crc_g,    (void*)&aux};
     if (stamps && !t.fn_stamps) return hipErrorInvalidValue;
+#if PL_TREE_DYN
+    // the frame-group counter (kernel: group loop)
+    if (hipError_t e = hipMemsetAsync(ws - kTreeSchedBytes, 0, 4, s); e != hipSuccess) return e;
+#endif
     return hipLaunchKernel(stamps ? t.fn_stamps : t.fn, dim3((unsigned)grid), dim3(64), args, t.lds_bytes, s);
 }
 

@@ -76,6 +76,24 @@ def summarise(src):
     return summ
 
 
+def launches(path):
+    """Per kernel from the rocprofv3 kernel trace: launches, mean over all of
+    them (what run_kernel_stats.csv averages: the bench's warmup launches
+    included) and over the bench's timed launches (the last 10 of the 12 that
+    --steps 10 --warmup 2 makes; the last n-1 of a key capped by
+    --extra-steps), the figure bench.py's HIP-event kernel_ms measures."""
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].replace("void ", "").split("(")[0]
+        d[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    out = {}
+    for name, t in d.items():
+        timed = t[-10:] if len(t) > 10 else t[1:] or t
+        out[name] = dict(launches=len(t), mean_ms_all=sum(t) / len(t), mean_ms_timed=sum(timed) / len(timed),
+                         timed_launches=len(timed), ms=[round(x, 4) for x in t])
+    return out
+
+
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     groups = sorted(g for g in os.listdir(src) if os.path.isdir(os.path.join(src, g, "trace")))
@@ -83,6 +101,8 @@ def main(src, dst):
     for g in groups:
         gs = os.path.join(src, g)
         shutil.copy(os.path.join(gs, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats_%s.csv" % g))
+        json.dump(launches(os.path.join(gs, "trace", "run_kernel_trace.csv")),
+                  open(os.path.join(dst, "kernel_launches_%s.json" % g), "w"), indent=1, sort_keys=True)
         if os.path.exists(os.path.join(gs, "bench_trace.json")):
             shutil.copy(os.path.join(gs, "bench_trace.json"), os.path.join(dst, "bench_trace_%s.json" % g))
         allsumm[g] = summarise(gs)

@@ -56,6 +56,12 @@ namespace {
 #ifndef PL_TREE_DYN
 #define PL_TREE_DYN 1  // frame groups past the first claimed from a counter (the kernel's group loop)
 #endif
+#ifndef PL_TREE_PRIO
+// issue priority (s_setprio) against the SIMD's age-ordered arbitration: 1 =
+// a group claimed in the last quarters of its round runs at priority 1..3;
+// 2 = also the first group by dispatch quarter (kernel: group loop)
+#define PL_TREE_PRIO 2
+#endif
 #ifndef PL_RATE0
 #define PL_RATE0 2  // rate-0 nodes of 2..8 leaves decoded at their first leaf; >= 2: metric chains per group
 #endif
@@ -679,6 +685,19 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
 #if PL_TREE_DYN
     unsigned int* const sched = reinterpret_cast<unsigned int*>(workspace - kTreeSchedBytes);
 #endif
+    // (not at n = 12, whose launches are bound by memory bandwidth: +3 % at
+    // 131 072 frames, profiles/r04_a/ab_prio_4096.log)
+    constexpr int PRIO = G::n <= 11 ? PL_TREE_PRIO : 0;
+#if PL_TREE_PRIO >= 2
+    if constexpr (PRIO >= 2) {
+        // the first group: later-dispatched wavefronts (younger on their SIMD,
+        // so behind in the age-ordered issue arbitration) start at a higher priority
+        const unsigned int q = blockIdx.x * 4u / gridDim.x;
+        if (q == 3) __builtin_amdgcn_s_setprio(3);
+        else if (q == 2) __builtin_amdgcn_s_setprio(2);
+        else if (q == 1) __builtin_amdgcn_s_setprio(1);
+    }
+#endif
     for (int64_t grp = blockIdx.x; grp < ngrp;) {
         const int64_t f0 = grp * FPW;
         const int64_t frame = f0 + fw;
@@ -1183,6 +1202,17 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         }
         nx = (unsigned int)__builtin_amdgcn_readfirstlane((int)nx);
         grp = nx == 0xFFFFFFFFu ? ngrp : (int64_t)gridDim.x + (int64_t)nx;
+#if PL_TREE_PRIO
+        // claims come in finishing order: a wavefront in the last quarters of
+        // its round runs the next group at a higher issue priority
+        if (PRIO >= 1 && nx != 0xFFFFFFFFu) {
+            const unsigned int q = (nx % gridDim.x) * 4u / gridDim.x;
+            if (q == 3) __builtin_amdgcn_s_setprio(3);
+            else if (q == 2) __builtin_amdgcn_s_setprio(2);
+            else if (q == 1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
 #else
         grp += gridDim.x;
 #endif

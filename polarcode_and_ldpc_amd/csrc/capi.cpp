@@ -242,7 +242,7 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
             return hipfail(e, "NaN redo kernel prepare");
         }
     }
-    p->head_bytes = p->mask_bytes + (p->tree ? (size_t)pl::kTreeSchedBytes : 0);
+    p->head_bytes = p->mask_bytes + (p->generic ? 0 : (size_t)pl::kSchedBytes);
     *out = p;
     return PL_OK;
 }
@@ -387,8 +387,8 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
 
 // Polar workspace layout for a grid of `grid` resident wavefronts: a list
 // plan's NaN masks first (for its largest grid, so they stay in place, and
-// zero, from one decode to the next), then the tree kernel's frame-group
-// counter (zeroed by tree_launch before each launch), then the list kernel's
+// zero, from one decode to the next), then the tree / lane kernel's frame-group
+// counter (zeroed by tree_launch / lane_launch before each launch), then the list kernel's
 // slices, which the NaN redo kernel reuses as its scratch once the list kernel
 // is done.
 static size_t polar_bytes(const pl_plan* p, int64_t grid) {
@@ -433,7 +433,7 @@ static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld,
         while (grid > 1 && polar_bytes(p, grid) > ws_bytes) grid = std::min<int64_t>(grid - 1, grid * ws_bytes / polar_bytes(p, grid));
         unsigned char* const base = (unsigned char*)ws;
         uint64_t* const masks = p->mask_bytes ? (uint64_t*)base : nullptr;
-        unsigned char* const slices = base + p->head_bytes;  // the tree kernel's counter: slices - kTreeSchedBytes
+        unsigned char* const slices = base + p->head_bytes;  // the group counter: slices - kSchedBytes
         if (masks && zero_masks) {  // a caller-owned workspace: the masks may hold anything
             hipError_t e = hipMemsetAsync(masks, 0, (size_t)grid * 8 * pl::kNanMaskPasses, s);
             if (e != hipSuccess) return hipfail(e, "NaN mask reset");

@@ -44,10 +44,10 @@ struct TreeInfo {
     int F, DL, fpw;
 };
 bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info);
-// The tree kernel's frame groups (FPW frames) past the first one per wavefront
-// come from a u32 counter in the kTreeSchedBytes just before its slices
-// (PL_TREE_DYN, polar_tree.hip); tree_launch zeroes it.
-constexpr int kTreeSchedBytes = 4096;
+// The tree and lane kernels' frame groups (FPW frames) past the first one per
+// wavefront come from a u32 counter in the kSchedBytes just before their
+// slices (polar_tree.hip, polar_lane.hpp); tree_launch / lane_launch zero it.
+constexpr int kSchedBytes = 4096;
 hipError_t tree_prepare(const TreeInfo& t, int* max_blocks_per_cu);
 hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t* out, const uint32_t* frozen_dec,
                        const int32_t* info_pos, int64_t batch, int K, int Lsz, unsigned char* ws, int grid,

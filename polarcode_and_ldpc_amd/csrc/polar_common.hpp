@@ -94,4 +94,15 @@ PL_DEV uint32_t crc_of_xhat(const uint32_t* root, int stride, int words, const u
     return crc;
 }
 
+// Issue priority 0..3 by the quarter of [0, n) that i falls in (the list
+// kernels' frame-group schedule, polar_tree.hip / polar_lane.hpp): s_setprio
+// takes an immediate, so one branch per level (wave-uniform).
+PL_DEV void set_prio_quarter(unsigned int i, unsigned int n) {
+    const unsigned int q = (unsigned int)(((uint64_t)i * 4u) / n);
+    if (q >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (q == 2) __builtin_amdgcn_s_setprio(2);
+    else if (q == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
 }  // namespace pl

@@ -93,6 +93,8 @@ hipError_t lane_launch(const LaneGeom& g, bool sc, const double* llr, int64_t ld
     LaneGeom gg = g;
     void* args[] = {&gg,           (void*)&llr,   (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos,
                     (void*)&batch, (void*)&ws,    (void*)&crc_g, (void*)&nan_masks};
+    // the frame-group counter (polar_lane.hpp: group loop)
+    if (hipError_t e = hipMemsetAsync(ws - kSchedBytes, 0, 4, s); e != hipSuccess) return e;
     return hipLaunchKernel(k, dim3((unsigned)grid), dim3((unsigned)g.lw), args, g.lds_bytes, s);
 }
 

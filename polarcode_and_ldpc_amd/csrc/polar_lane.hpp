@@ -204,6 +204,14 @@ PL_DEV double fused_top(const Ctx& c, int i, const double* __restrict__ ch, cons
 
 }  // namespace
 
+#ifndef PL_LANE_DYN_LCAP
+#define PL_LANE_DYN_LCAP 1024  // list capacities whose frame groups come from the counter
+#endif
+#ifndef PL_LANE_PRIO_LCAP
+// ... and run at issue priorities by dispatch / claim order (up to 32: at 64 and
+// 128 +2 / +5 %, equal without; profiles/r04_a/ab_lane_dyn2.log)
+#define PL_LANE_PRIO_LCAP 32
+#endif
 // LCAP <= 64: 64/LCAP frames per wavefront, list exchanges by ds_bpermute.
 // LCAP > 64: one frame per workgroup of LCAP lanes (LCAP/64 wavefronts), list
 // exchanges through LDS (g.lds_xchg) behind workgroup barriers.
@@ -229,8 +237,19 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
     c.base = fw * LCAP;
     c.lw = LW;
 
-    int pass = 0;
-    for (int64_t f0 = (int64_t)blockIdx.x * FPW; f0 < batch; f0 += (int64_t)gridDim.x * FPW, ++pass) {
+    // Frame groups as in polar_tree.hip: group blockIdx.x first, every later
+    // one from the workspace counter (kSchedBytes before the slices, zeroed by
+    // lane_launch); issue priority by dispatch quarter, then by claim order
+    // (the SIMD's age-ordered arbitration otherwise makes its youngest
+    // wavefront the launch's tail).  NaN mask word of group grp: [grp % grid][grp / grid].
+    const int64_t ngrp = (batch + FPW - 1) / FPW;
+    constexpr bool DYN = LCAP <= PL_LANE_DYN_LCAP, PRIO = LCAP <= PL_LANE_PRIO_LCAP;
+    unsigned int* const sched = reinterpret_cast<unsigned int*>(workspace - kSchedBytes);
+    __shared__ unsigned int claim;
+    if constexpr (PRIO) set_prio_quarter(blockIdx.x, gridDim.x);
+    for (int64_t grp = blockIdx.x; grp < ngrp;) {
+        const int64_t f0 = grp * FPW;
+        const uint32_t pass = (uint32_t)(grp / gridDim.x), mwave = (uint32_t)(grp % gridDim.x);
         const int64_t frame = f0 + fw;
         const bool live = frame < batch;
         const double* __restrict__ ch = llr + (live ? frame : batch - 1) * ld;
@@ -450,16 +469,16 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
             nanf |= (slot < nact) & __builtin_isnan(pm);
             if constexpr (LCAP > 64) {
                 const bool any = __syncthreads_or(nanf);
-                if (nan_masks && pass < kNanMaskPasses && lane == 0)
-                    nan_masks[(size_t)blockIdx.x * kNanMaskPasses + pass] = any ? 1ull : 0ull;
+                if (nan_masks && pass < (uint32_t)kNanMaskPasses && lane == 0)
+                    nan_masks[(size_t)mwave * kNanMaskPasses + pass] = any ? 1ull : 0ull;
             } else {
                 const uint64_t bal = __ballot(nanf);
-                if (nan_masks && pass < kNanMaskPasses) {
+                if (nan_masks && pass < (uint32_t)kNanMaskPasses) {
                     constexpr uint64_t GM = LCAP >= 64 ? ~0ull : ((1ull << LCAP) - 1ull);
                     uint64_t fm = 0;
 #pragma unroll
                     for (int f = 0; f < FPW; ++f) fm |= (uint64_t)(((bal >> (f * LCAP)) & GM) != 0ull) << f;
-                    if (lane == 0) nan_masks[(size_t)blockIdx.x * kNanMaskPasses + pass] = fm;
+                    if (lane == 0) nan_masks[(size_t)mwave * kNanMaskPasses + pass] = fm;
                 }
             }
         }
@@ -530,7 +549,29 @@ polar_lane_kernel(LaneGeom g, const double* __restrict__ llr, int64_t ld, uint8_
                 o[k] = (uint8_t)((X[p >> 5] >> (p & 31)) & 1u);
             }
         }
-        __syncthreads();
+        if constexpr (!DYN) {
+            __syncthreads();
+            grp += gridDim.x;
+            continue;
+        }
+        // the next group (a counter read past the end skips the claim)
+        unsigned int nx = 0xFFFFFFFFu;
+        if (threadIdx.x == 0) {
+            const unsigned int seen = __hip_atomic_load(sched, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((int64_t)gridDim.x + (int64_t)seen < ngrp)
+                nx = __hip_atomic_fetch_add(sched, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if constexpr (LCAP > 64) claim = nx;
+        }
+        if constexpr (LCAP > 64) {
+            __syncthreads();
+            nx = claim;
+            __syncthreads();  // read by every wavefront before the next claim overwrites it
+        } else {
+            nx = (unsigned int)__builtin_amdgcn_readfirstlane((int)nx);
+            __syncthreads();
+        }
+        grp = nx == 0xFFFFFFFFu ? ngrp : (int64_t)gridDim.x + (int64_t)nx;
+        if (PRIO && nx != 0xFFFFFFFFu) set_prio_quarter(nx % gridDim.x, gridDim.x);
     }
 }
 

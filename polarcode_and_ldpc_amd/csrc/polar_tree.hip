@@ -677,26 +677,21 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
     }
 
     // Frame groups (FPW frames each): group blockIdx.x first; then, with
-    // PL_TREE_DYN, the next unclaimed group from one counter (kTreeSchedBytes
+    // PL_TREE_DYN, the next unclaimed group from one counter (kSchedBytes
     // before the slices, zeroed by tree_launch), so that wavefronts slowed by
     // harder frames, a busier SIMD or a busier XCD take fewer groups instead of
     // stretching the launch's tail; else groups b, b + grid, b + 2 grid, ...
     const int64_t ngrp = (batch + FPW - 1) / FPW;
 #if PL_TREE_DYN
-    unsigned int* const sched = reinterpret_cast<unsigned int*>(workspace - kTreeSchedBytes);
+    unsigned int* const sched = reinterpret_cast<unsigned int*>(workspace - kSchedBytes);
 #endif
     // (not at n = 12, whose launches are bound by memory bandwidth: +3 % at
     // 131 072 frames, profiles/r04_a/ab_prio_4096.log)
     constexpr int PRIO = G::n <= 11 ? PL_TREE_PRIO : 0;
 #if PL_TREE_PRIO >= 2
-    if constexpr (PRIO >= 2) {
-        // the first group: later-dispatched wavefronts (younger on their SIMD,
-        // so behind in the age-ordered issue arbitration) start at a higher priority
-        const unsigned int q = blockIdx.x * 4u / gridDim.x;
-        if (q == 3) __builtin_amdgcn_s_setprio(3);
-        else if (q == 2) __builtin_amdgcn_s_setprio(2);
-        else if (q == 1) __builtin_amdgcn_s_setprio(1);
-    }
+    // the first group: later-dispatched wavefronts (younger on their SIMD, so
+    // behind in the age-ordered issue arbitration) start at a higher priority
+    if constexpr (PRIO >= 2) set_prio_quarter(blockIdx.x, gridDim.x);
 #endif
     for (int64_t grp = blockIdx.x; grp < ngrp;) {
         const int64_t f0 = grp * FPW;
@@ -1205,13 +1200,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
 #if PL_TREE_PRIO
         // claims come in finishing order: a wavefront in the last quarters of
         // its round runs the next group at a higher issue priority
-        if (PRIO >= 1 && nx != 0xFFFFFFFFu) {
-            const unsigned int q = (nx % gridDim.x) * 4u / gridDim.x;
-            if (q == 3) __builtin_amdgcn_s_setprio(3);
-            else if (q == 2) __builtin_amdgcn_s_setprio(2);
-            else if (q == 1) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
+        if (PRIO >= 1 && nx != 0xFFFFFFFFu) set_prio_quarter(nx % gridDim.x, gridDim.x);
 #endif
 #else
         grp += gridDim.x;
@@ -1351,7 +1340,7 @@ hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t
     if (stamps && !t.fn_stamps) return hipErrorInvalidValue;
 #if PL_TREE_DYN
     // the frame-group counter (kernel: group loop)
-    if (hipError_t e = hipMemsetAsync(ws - kTreeSchedBytes, 0, 4, s); e != hipSuccess) return e;
+    if (hipError_t e = hipMemsetAsync(ws - kSchedBytes, 0, 4, s); e != hipSuccess) return e;
 #endif
     return hipLaunchKernel(stamps ? t.fn_stamps : t.fn, dim3((unsigned)grid), dim3(64), args, t.lds_bytes, s);
 }

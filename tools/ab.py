@@ -15,7 +15,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-CASES = ("polar_l8_128k", "polar_l32_64k", "polar_4096_128k", "polar_2048", "polar_l16", "polar_sc128", "polar_sc512", "polar_sc2048", "polar_sc4096", "polar_l8", "ldpc_bp", "ldpc_bp_valid", "polar_l32", "polar_4096", "ms_8192", "polar_sc", "polar_sc_def",
+CASES = ("lane_2048_l32", "lane_1024_l64", "lane_512_l4", "lane_8192_l8", "lane_1024_l128", "polar_l8_128k", "polar_l32_64k", "polar_4096_128k", "polar_2048", "polar_l16", "polar_sc128", "polar_sc512", "polar_sc2048", "polar_sc4096", "polar_l8", "ldpc_bp", "ldpc_bp_valid", "polar_l32", "polar_4096", "ms_8192", "polar_sc", "polar_sc_def",
          "polar_sc256")
 
 
@@ -48,9 +48,12 @@ def worker(cases):
         return int((x * w).sum().item())
 
     for case in cases:
-        if case.startswith("polar"):
+        if case.startswith("polar") or case.startswith("lane"):
             N, L, B, snr = {"polar_l8": (1024, 8, 65536, 3.0), "polar_l32": (1024, 32, 16384, 1.0), "polar_l32_64k": (1024, 32, 65536, 1.0),
                             "polar_l8_128k": (1024, 8, 131072, 3.0),
+                            "lane_2048_l32": (2048, 32, 16384, 1.0), "lane_1024_l64": (1024, 64, 8192, 1.0),
+                            "lane_512_l4": (512, 4, 65536, 2.0), "lane_8192_l8": (8192, 8, 8192, 2.0),
+                            "lane_1024_l128": (1024, 128, 4096, 1.0),
                             "polar_4096_128k": (4096, 8, 131072, 3.0), "polar_l16": (1024, 16, 32768, 1.0), "polar_2048": (2048, 8, 32768, 1.0),
                             "polar_4096": (4096, 8, 16384, 1.0), "polar_sc": (1024, 0, 65536, 3.0),
                             "polar_sc_def": (1024, 0, 65536, 3.0), "polar_sc256": (256, 0, 65536, 3.0),

@@ -236,6 +236,29 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
     if (iters && tid == 0) iters[frame] = done;
 }
 
+#ifndef PL_MS_PRIO
+// ldpc_ms_compact_kernel: issue priority falling with a wavefront's progress
+// through each pass (16 384 frames of n = 8192: 12.61 -> 11.78 ms,
+// profiles/r04_a/ab_bp_prio.log)
+#define PL_MS_PRIO 1
+#endif
+// s_setprio 3..0 as step i of n passes its quarters: the wavefronts of a SIMD
+// belong to one workgroup and meet at the next barrier, so the ones behind
+// get the issue slots (age-ordered arbitration otherwise lets the oldest run ahead)
+PL_DEV void ms_prio(int i, int n) {
+    const int q = (4 * i) / n;
+    if (q == 0) __builtin_amdgcn_s_setprio(3);
+    else if (q == 1) __builtin_amdgcn_s_setprio(2);
+    else if (q == 2) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
+#ifndef PL_BP_PRIO
+// the same in ldpc_reg_kernel: +1.4 % (its SIMDs hold one wavefront of each of
+// four workgroups, which need not keep pace with each other), off
+#define PL_BP_PRIO 0
+#endif
+
 // Register-cached variant of ldpc_decode_kernel for codes whose variable degree
 // is a constant DV < 8 (np.sum is then sequential) and whose state fits LDS:
 // 256 threads, thread tid owns edges tid + j*256 (j < EPT) and variables
@@ -319,6 +342,7 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         for (int c = tid; c < m; c += NT) scur[c] = 0u;
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
+            if constexpr (PL_BP_PRIO) ms_prio(j, EPT);
             const int e = tid + j * NT;
             if (e >= E) break;
             const int e0 = meta[j] & 0xFFFFF, d = meta[j] >> 20, i = e - e0;
@@ -390,6 +414,7 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         int wn = 0;                                                 // its length (wavefront-uniform)
 #pragma unroll
         for (int j = 0; j < VPT; ++j) {
+            if constexpr (PL_BP_PRIO) ms_prio(j, VPT);
             const int v = tid + j * NT;
             const bool vok = v < n;  // lanes past n run along (ve = 0) with every store masked
             if (!__ballot(vok)) break;
@@ -666,6 +691,7 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
             constexpr int CB = PL_MS_CB < MQ ? (PL_MS_CB > 0 ? PL_MS_CB : 1) : MQ;
 #pragma unroll
             for (int q0 = 0; q0 < MQ; q0 += CB) {
+                if constexpr (PL_MS_PRIO) ms_prio(q0, MQ);
                 double2 om[CB];
                 uint32_t ometa[CB];
                 double tv[CB][DC];
@@ -756,6 +782,7 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
             constexpr int VB = PL_MS_VB < VPT ? (PL_MS_VB > 0 ? PL_MS_VB : 1) : VPT;
 #pragma unroll
             for (int j0 = 0; j0 < VPT; j0 += VB) {
+                if constexpr (PL_MS_PRIO) ms_prio(j0, VPT);
                 double2 mm[VB][DV];
                 uint32_t mt[VB][DV];
                 int pos[VB][DV];

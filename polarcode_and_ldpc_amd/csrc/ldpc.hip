@@ -238,9 +238,10 @@ ldpc_decode_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
 
 #ifndef PL_MS_PRIO
 // ldpc_ms_compact_kernel: issue priority falling with a wavefront's progress
-// through each pass (16 384 frames of n = 8192: 12.61 -> 11.78 ms,
-// profiles/r04_a/ab_bp_prio.log)
-#define PL_MS_PRIO 1
+// through each pass, 1 = per batch of checks, 2 = per check (16 384 frames of
+// n = 8192: 12.61 -> 11.78 -> 11.40 ms, profiles/r04_a/ab_bp_prio.log,
+// ab_ms_prio2.log)
+#define PL_MS_PRIO 2
 #endif
 // s_setprio 3..0 as step i of n passes its quarters: the wavefronts of a SIMD
 // belong to one workgroup and meet at the next barrier, so the ones behind
@@ -691,7 +692,7 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
             constexpr int CB = PL_MS_CB < MQ ? (PL_MS_CB > 0 ? PL_MS_CB : 1) : MQ;
 #pragma unroll
             for (int q0 = 0; q0 < MQ; q0 += CB) {
-                if constexpr (PL_MS_PRIO) ms_prio(q0, MQ);
+                if constexpr (PL_MS_PRIO == 1) ms_prio(q0, MQ);
                 double2 om[CB];
                 uint32_t ometa[CB];
                 double tv[CB][DC];
@@ -707,6 +708,7 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
                 }
 #pragma unroll
                 for (int b = 0; b < CB; ++b) {
+                    if constexpr (PL_MS_PRIO >= 2) ms_prio(q0 + b, MQ);
                     const int c = tid + 1024 * (q0 + b);
                     if (q0 + b >= MQ || c >= m) continue;
                     double x[DC];

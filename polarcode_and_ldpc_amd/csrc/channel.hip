@@ -113,14 +113,26 @@ gf2_encode_kernel(const uint32_t* __restrict__ g, int k, int n, const uint8_t* _
 // two LLRs per thread (one Philox call -> two 53-bit uniforms -> Box-Muller
 // pair); with even n and ld and aligned rows (vec) one 2-byte codeword load and
 // one 16-byte LLR store per thread
+// ROWS: a 2-D grid, blockIdx.x = the frame (b0 + blockIdx.x), blockIdx.y *
+// blockDim.x + threadIdx.x = the pair (rows of >= 128 pairs: no 64-bit
+// division per thread); otherwise flat over batch * pairs from `base`.
+template <bool ROWS>
 __global__ void awgn_kernel(const uint8_t* __restrict__ cw, int n, int64_t batch, double sigma,
                             double sigma2, uint64_t seed, int64_t off, double* __restrict__ llr, int64_t ld,
                             int vec, int64_t base) {
     const int ppf = (n + 1) / 2;
-    const int64_t idx = base + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= batch * ppf) return;
-    const int64_t b = idx / ppf;
-    const int q = (int)(idx % ppf);
+    int64_t b;
+    int q;
+    if constexpr (ROWS) {
+        b = base + blockIdx.x;
+        q = (int)(blockIdx.y * blockDim.x + threadIdx.x);
+        if (q >= ppf) return;
+    } else {
+        const int64_t idx = base + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (idx >= batch * ppf) return;
+        b = idx / ppf;
+        q = (int)(idx % ppf);
+    }
     const uint64_t f = (uint64_t)(off + b);
     const pl_u4 r = philox4x32_10(pl_u4{(uint32_t)q, (uint32_t)f, (uint32_t)(f >> 32), 0xA3A3A3A3u},
                                   (uint32_t)seed ^ 0x5bd1e995u, (uint32_t)(seed >> 32));
@@ -329,9 +341,23 @@ hipError_t gf2_encode_launch(const uint32_t* g, int k, int n, const uint8_t* msg
 hipError_t awgn_launch(const uint8_t* cw, int n, int64_t batch, double sigma, double sigma2, uint64_t seed,
                        int64_t off, double* llr, int64_t ld, hipStream_t s) {
     const int vec = (n % 2 == 0) && (ld % 2 == 0) && (((uintptr_t)llr & 15) == 0) && (((uintptr_t)cw & 1) == 0);
-    return chunked(batch * ((n + 1) / 2), [&](dim3 grid, int64_t base) {
-        hipLaunchKernelGGL(awgn_kernel, grid, dim3(256), 0, s, cw, n, batch, sigma, sigma2, seed, off, llr, ld, vec,
-                           base);
+    const int ppf = (n + 1) / 2;
+    if (ppf >= 128) {
+        const int t = ppf >= 256 ? 256 : 128;
+        const unsigned gy = (unsigned)((ppf + t - 1) / t);
+        const int64_t fmax = (int64_t)1 << 24;  // frames per launch (grid x)
+        for (int64_t b0 = 0; b0 < batch; b0 += fmax) {
+            const int64_t nf = batch - b0 < fmax ? batch - b0 : fmax;
+            hipLaunchKernelGGL(awgn_kernel<true>, dim3((unsigned)nf, gy), dim3(t), 0, s, cw, n, batch, sigma, sigma2,
+                               seed, off, llr, ld, vec, b0);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    return chunked(batch * ppf, [&](dim3 grid, int64_t base) {
+        hipLaunchKernelGGL(awgn_kernel<false>, grid, dim3(256), 0, s, cw, n, batch, sigma, sigma2, seed, off, llr, ld,
+                           vec, base);
     });
 }
 

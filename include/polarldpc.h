@@ -96,7 +96,10 @@ int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr, const int3
  *             word (decoded = total <= 0).
  *   iters_dev: int32 [batch] device or NULL; LDPC: iterations run (BPDecoder's
  *             return_iterations); polar: ignored.
- *   Asynchronous on `stream`.  Deterministic (no atomics in the decode path).
+ *   Asynchronous on `stream`.  Deterministic bits: the decode path's atomics
+ *   (the polar list kernels' frame-group counter and NaN mask ORs, LDPC
+ *   syndrome XORs in LDS) decide which wavefront decodes which frames, never
+ *   what a frame decodes to.
  *   Workspace: the plan keeps one device buffer per stream, sized on first use
  *   to this batch (polar: one slice per resident wavefront, at most the
  *   persistent grid; LDPC codes whose messages exceed LDS: one per frame of a

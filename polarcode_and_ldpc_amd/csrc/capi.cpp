@@ -45,7 +45,6 @@ struct pl_plan {
     int list_size = 0;
     uint32_t* d_frozen_dec = nullptr;  // decode-order frozen bitmask [ceil(N/32)]
     int32_t* d_info_pos = nullptr;     // [K] ascending info indices
-    int32_t* d_pos2info = nullptr;     // [N] index -> info rank or -1
     uint32_t* d_crc_g = nullptr;       // CA-SCL: CRC contribution of x_hat bit j [N] (null = plain SCL)
     uint32_t* d_r0k = nullptr;         // SC tree kernel: log2 size of the largest all-frozen node at leaf i (4-bit fields)
     std::vector<int32_t> h_info;       // ascending info positions (host copy)
@@ -144,9 +143,9 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
     if (!frozen_mask) return fail(PL_EINVAL, "frozen_mask is NULL");
     int n = 0;
     while ((1 << n) < N) ++n;
-    std::vector<int32_t> info, pos2info(N, -1);
+    std::vector<int32_t> info;
     for (int j = 0; j < N; ++j)
-        if (!frozen_mask[j]) { pos2info[j] = (int32_t)info.size(); info.push_back(j); }
+        if (!frozen_mask[j]) info.push_back(j);
     if ((int)info.size() != K) return fail(PL_EINVAL, "number of unfrozen positions != K");
     std::vector<uint32_t> fdec((N + 31) / 32, 0u);
     for (int i = 0; i < N; ++i)
@@ -167,8 +166,7 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
     p->tree = !p->generic && !(kern && std::string(kern) == "lane") && !(flags & 0x3F) &&
               pl::tree_lookup(n, lcap, p->sc, &p->tinfo);
     hipError_t e;
-    if ((e = upload(&p->d_frozen_dec, fdec)) != hipSuccess || (e = upload(&p->d_info_pos, info)) != hipSuccess ||
-        (e = upload(&p->d_pos2info, pos2info)) != hipSuccess) {
+    if ((e = upload(&p->d_frozen_dec, fdec)) != hipSuccess || (e = upload(&p->d_info_pos, info)) != hipSuccess) {
         pl_plan_destroy(p);
         return hipfail(e, "plan upload");
     }
@@ -728,7 +726,6 @@ extern "C" int pl_plan_destroy(pl_plan* p) {
     if (!p) return PL_OK;
     if (p->d_frozen_dec) hipFree(p->d_frozen_dec);
     if (p->d_info_pos) hipFree(p->d_info_pos);
-    if (p->d_pos2info) hipFree(p->d_pos2info);
     if (p->d_crc_g) hipFree(p->d_crc_g);
     if (p->d_r0k) hipFree(p->d_r0k);
     if (p->d_ldpc) hipFree(p->d_ldpc);
@@ -751,7 +748,7 @@ extern "C" int pl_polar_encode(const pl_plan* p, const uint8_t* msg, int64_t bat
     const int64_t step = kMaxLaunchItems / 64;  // one wavefront per frame
     for (int64_t b0 = 0; b0 < batch; b0 += step) {
         const int64_t nb = std::min<int64_t>(step, batch - b0);
-        hipError_t e = pl::polar_encode_launch(p->pg.N, p->pg.K, p->d_pos2info, msg + b0 * p->pg.K, nb,
+        hipError_t e = pl::polar_encode_launch(p->pg.N, p->pg.K, p->d_info_pos, msg + b0 * p->pg.K, nb,
                                                cw + b0 * p->pg.N, (hipStream_t)stream);
         if (e != hipSuccess) return hipfail(e, "polar encode launch");
     }

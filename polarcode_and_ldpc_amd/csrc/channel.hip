@@ -40,40 +40,65 @@ __global__ void random_bits_kernel(uint64_t seed, int64_t off, int64_t batch, in
     for (int j = 0; j < cnt; ++j) o[j] = (x >> j) & 1u;
 }
 
-// one wavefront per frame: u by ballot over N positions, transform in LDS.
-__global__ void __launch_bounds__(64)
-polar_encode_kernel(int N, int K, const int32_t* __restrict__ pos2info, const uint8_t* __restrict__ msg,
+// one wavefront per frame, four frames per workgroup (each wavefront its own
+// LDS words, no workgroup barrier): u scattered into LDS words from the
+// message (4 bytes per lane per load on aligned rows, an LDS OR per set bit at
+// its info position), transform in LDS, then 4 codeword bytes per lane per
+// store (aligned rows; else bytes).
+__global__ void __launch_bounds__(256)
+polar_encode_kernel(int N, int K, const int32_t* __restrict__ info_pos, const uint8_t* __restrict__ msg,
                     int64_t batch, uint8_t* __restrict__ cw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t* X = reinterpret_cast<uint32_t*>(smem);
-    const int64_t b = blockIdx.x;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + wv;
     if (b >= batch) return;
-    const int lane = threadIdx.x;
     const int words = N < 32 ? 1 : N / 32;
+    uint32_t* X = reinterpret_cast<uint32_t*>(smem) + wv * (words + 2);
     const uint8_t* m = msg + b * K;
-    for (int base = 0; base < N; base += 64) {
-        const int j = base + lane;
-        int bitv = 0;
-        if (j < N) {
-            const int k = pos2info[j];
-            bitv = (k >= 0) ? (m[k] & 1) : 0;
+    for (int w = lane; w < words; w += 64) X[w] = 0u;
+    // LDS runs a wavefront's operations in order: only compiler reordering to stop
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if ((K & 3) == 0 && ((uintptr_t)m & 3) == 0) {
+        for (int k0 = 4 * lane; k0 < K; k0 += 256) {
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(m + k0);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if ((v >> (8 * t)) & 1u) {
+                    const int p = info_pos[k0 + t];
+                    atomicOr(&X[p >> 5], 1u << (p & 31));
+                }
+            }
         }
-        const unsigned long long bal = __ballot(bitv);
-        if (lane == 0) {
-            X[base / 32] = (uint32_t)bal;
-            if (base / 32 + 1 < words) X[base / 32 + 1] = (uint32_t)(bal >> 32);
+    } else {
+        for (int k = lane; k < K; k += 64) {
+            if (m[k] & 1) {
+                const int p = info_pos[k];
+                atomicOr(&X[p >> 5], 1u << (p & 31));
+            }
         }
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     for (int w = lane; w < words; w += 64) X[w] = polar_word_transform(X[w]);
     for (int sw = 1; sw < words; sw <<= 1) {
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
         for (int w = lane; w < words; w += 64)
             if (!(w & sw)) X[w] ^= X[w + sw];
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     uint8_t* o = cw + b * N;
-    for (int j = lane; j < N; j += 64) o[j] = (X[j >> 5] >> (j & 31)) & 1u;
+    if ((N & 3) == 0 && ((uintptr_t)o & 3) == 0) {
+        uint32_t* o4 = reinterpret_cast<uint32_t*>(o);
+        for (int q = lane; q < N / 4; q += 64) {
+            const uint32_t x = (X[q >> 3] >> ((q & 7) * 4)) & 15u;  // bits 4q .. 4q+3
+            o4[q] = (x & 1u) | ((x & 2u) << 7) | ((x & 4u) << 14) | ((x & 8u) << 21);
+        }
+    } else {
+        for (int j = lane; j < N; j += 64) o[j] = (X[j >> 5] >> (j & 31)) & 1u;
+    }
 }
 
 // GF(2) block encoder (LDPC valid-codeword encoding, SURVEY §8 f row 3; the
@@ -320,12 +345,12 @@ hipError_t random_bits_launch(uint64_t seed, int64_t off, int64_t batch, int k, 
     });
 }
 
-hipError_t polar_encode_launch(int N, int K, const int32_t* pos2info, const uint8_t* msg, int64_t batch,
+hipError_t polar_encode_launch(int N, int K, const int32_t* info_pos, const uint8_t* msg, int64_t batch,
                                uint8_t* cw, hipStream_t s) {
     if (batch == 0) return hipSuccess;
     const int words = N < 32 ? 1 : N / 32;
-    hipLaunchKernelGGL(polar_encode_kernel, dim3((unsigned)batch), dim3(64), words * 4 + 8, s, N, K, pos2info,
-                       msg, batch, cw);
+    hipLaunchKernelGGL(polar_encode_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 4 * (words + 2) * 4, s, N,
+                       K, info_pos, msg, batch, cw);
     return hipGetLastError();
 }
 

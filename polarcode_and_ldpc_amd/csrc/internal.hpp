@@ -79,7 +79,7 @@ hipError_t fpw_launch(const double* llr, int64_t ld, uint8_t* out, const uint32_
                       hipStream_t st);
 #endif
 
-hipError_t polar_encode_launch(int N, int K, const int32_t* pos2info, const uint8_t* msg,
+hipError_t polar_encode_launch(int N, int K, const int32_t* info_pos, const uint8_t* msg,
                                int64_t batch, uint8_t* cw, hipStream_t s);
 hipError_t random_bits_launch(uint64_t seed, int64_t off, int64_t batch, int k, uint8_t* bits,
                               hipStream_t s);

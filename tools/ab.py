@@ -15,7 +15,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-CASES = ("awgn_1024", "awgn_8192", "lane_2048_l32", "lane_1024_l64", "lane_512_l4", "lane_8192_l8", "lane_1024_l128", "polar_l8_128k", "polar_l32_64k", "polar_4096_128k", "polar_2048", "polar_l16", "polar_sc128", "polar_sc512", "polar_sc2048", "polar_sc4096", "polar_l8", "ldpc_bp", "ldpc_bp_valid", "polar_l32", "polar_4096", "ms_8192", "polar_sc", "polar_sc_def",
+CASES = ("enc_1024", "enc_4096", "awgn_1024", "awgn_8192", "lane_2048_l32", "lane_1024_l64", "lane_512_l4", "lane_8192_l8", "lane_1024_l128", "polar_l8_128k", "polar_l32_64k", "polar_4096_128k", "polar_2048", "polar_l16", "polar_sc128", "polar_sc512", "polar_sc2048", "polar_sc4096", "polar_l8", "ldpc_bp", "ldpc_bp_valid", "polar_l32", "polar_4096", "ms_8192", "polar_sc", "polar_sc_def",
          "polar_sc256")
 
 
@@ -98,6 +98,18 @@ def worker(cases):
             its = torch.empty((B,), dtype=torch.int32, device="cuda")
             ms = timeit(lambda: plan.decode(llr, out, its))
             res[case] = dict(ms=ms, digest=digest(out) ^ digest(its))
+        elif case.startswith("enc_"):
+            N = int(case.split("_")[1])
+            K, B = N // 2, 65536 if N <= 1024 else 16384
+            fr = construct_frozen_set(N, K, 2.0)
+            mask = np.zeros(N, np.uint8)
+            mask[fr] = 1
+            plan = _native.polar_plan(N, K, mask, 8)
+            msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+            _native.random_bits(3, 0, msg)
+            cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+            ms = timeit(lambda: _native.polar_encode(plan, msg, cw))
+            res[case] = dict(ms=ms, digest=digest(cw))
         elif case.startswith("awgn_"):
             n = int(case.split("_")[1])
             B = 65536 if n <= 1024 else 16384

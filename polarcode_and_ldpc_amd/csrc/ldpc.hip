@@ -275,15 +275,27 @@ PL_DEV void ms_prio(int i, int n) {
 #ifndef PL_LDPC_REG_WPE
 #define PL_LDPC_REG_WPE 4  // waves per SIMD the register budget is built for
 #endif
-template <int ALGO, int DV, int EPT, int VPT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PL_LDPC_REG_WPE)))
+// FPB > 1 (diagnostic, PL_BP_FPB): FPB frames per workgroup of 256 FPB threads
+// sharing its barriers, each frame with its own LDS (g.lds_bytes apart), a
+// per-frame early-stop vote in LDS after them, frames past the batch decoding
+// the last frame again (same bytes written twice).
+template <int ALGO, int DV, int EPT, int VPT, int FPB = 1>
+__global__ void __launch_bounds__(256 * FPB) __attribute__((amdgpu_waves_per_eu(PL_LDPC_REG_WPE)))
 ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
                 uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
     constexpr int NT = 256;
-    const int64_t frame = blockIdx.x;
-    if (frame >= batch) return;
-    const int tid = threadIdx.x;
+    const int fs = FPB > 1 ? (int)(threadIdx.x >> 8) : 0;
+    int64_t frame = (int64_t)blockIdx.x * FPB + fs;
+    if constexpr (FPB == 1) {
+        if (frame >= batch) return;
+    } else {
+        frame = frame < batch ? frame : batch - 1;
+    }
+    const int tid = FPB > 1 ? (int)(threadIdx.x & 255u) : (int)threadIdx.x;
+    unsigned char* const smem = smem_all + (size_t)fs * (size_t)g.lds_bytes;
+    unsigned int* const vote = reinterpret_cast<unsigned int*>(smem_all + (size_t)FPB * (size_t)g.lds_bytes);  // [2][FPB]
+    bool fdone = false;
     const int E = g.E, n = g.n, m = g.m;
     double* T = reinterpret_cast<double*>(smem);
     double* C = T + E;
@@ -319,6 +331,9 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         chv[j] = ok ? ch[v] : 0.0;
     }
     for (int c = tid; c < 2 * m; c += NT) syn[c] = 0u;
+    if constexpr (FPB > 1) {
+        if (threadIdx.x < 2 * FPB) vote[threadIdx.x] = 0u;
+    }
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
         if (tid + j * NT < n) {
@@ -337,12 +352,29 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         uint32_t* scur = syn + (it & 1) * m;
         if (g.early_stop && it > 0) {
             int bad = 0;
-            for (int c = tid; c < m; c += NT) bad |= (int)sprev[c];
-            if (!__syncthreads_or(bad)) { done = it; break; }
+            if (!fdone)
+                for (int c = tid; c < m; c += NT) bad |= (int)sprev[c];
+            if constexpr (FPB == 1) {
+                if (!__syncthreads_or(bad)) { done = it; break; }
+            } else {
+                // per-frame vote: a frame whose checks all hold stops at `it`
+                // and idles (its decisions kept) until every frame has stopped
+                if (__ballot(bad) && __lane_id() == 0) atomicOr(&vote[(it & 1) * FPB + fs], 1u);
+                __syncthreads();
+                unsigned int anyb = 0;
+#pragma unroll
+                for (int f = 0; f < FPB; ++f) anyb |= vote[(it & 1) * FPB + f];
+                const bool fb = vote[(it & 1) * FPB + fs] != 0u;
+                if (threadIdx.x < FPB) vote[((it + 1) & 1) * FPB + threadIdx.x] = 0u;
+                if (!fb && !fdone) { fdone = true; done = it; }
+                if (!anyb) break;
+            }
         }
+        if (!fdone)
         for (int c = tid; c < m; c += NT) scur[c] = 0u;
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
+            if (fdone) break;
             if constexpr (PL_BP_PRIO) ms_prio(j, EPT);
             const int e = tid + j * NT;
             if (e >= E) break;
@@ -415,6 +447,7 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         int wn = 0;                                                 // its length (wavefront-uniform)
 #pragma unroll
         for (int j = 0; j < VPT; ++j) {
+            if (fdone) break;
             if constexpr (PL_BP_PRIO) ms_prio(j, VPT);
             const int v = tid + j * NT;
             const bool vok = v < n;  // lanes past n run along (ve = 0) with every store masked
@@ -454,7 +487,7 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
             // runs a wavefront's operations in order: no barrier
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            for (int w = lane; w < wn; w += 64) {
+            for (int w = lane; w < wn; w += 64) {  // wn = 0 for a stopped frame
                 const int e = wl[w];
 #if PL_DIAG && defined(PL_ABL_TANH)
                 T[e] = 0.5 * T[e];  // ablation timing build: no tanh
@@ -472,6 +505,13 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
 
 // (DV, EPT, VPT) instances of ldpc_reg_kernel: E <= 256*EPT, n <= 256*VPT
 struct RegVariant { int dv, ept, vpt; void* k[2]; };
+#if PL_DIAG
+static void* reg_fpb_kernel(int fpb, int algo) {  // diagnostic FPB instances of the (3, 6, 2) variant
+    if (fpb == 2) return algo == 0 ? (void*)ldpc_reg_kernel<0, 3, 6, 2, 2> : (void*)ldpc_reg_kernel<1, 3, 6, 2, 2>;
+    if (fpb == 4) return algo == 0 ? (void*)ldpc_reg_kernel<0, 3, 6, 2, 4> : (void*)ldpc_reg_kernel<1, 3, 6, 2, 4>;
+    return nullptr;
+}
+#endif
 template <int DV, int EPT, int VPT>
 static RegVariant reg_variant() {
     return {DV, EPT, VPT, {(void*)ldpc_reg_kernel<0, DV, EPT, VPT>, (void*)ldpc_reg_kernel<1, DV, EPT, VPT>}};
@@ -996,7 +1036,20 @@ static void* pick_kernel(const LdpcGeom& g) {
     return g.algo == 0 ? pick<0>(g.use_global) : pick<1>(g.use_global);
 }
 
+#if PL_DIAG
+static int bp_fpb(const LdpcGeom& g) {  // PL_BP_FPB=2|4: the reg (3, 6, 2) variant with FPB frames per workgroup
+    static const int v = [] { const char* e = std::getenv("PL_BP_FPB"); return e ? std::atoi(e) : 1; }();
+    return (v == 2 || v == 4) && g.reg_variant == 1 ? v : 1;
+}
+static size_t fpb_lds(const LdpcGeom& g, int f) { return (size_t)f * (((size_t)g.lds_bytes + 15) & ~(size_t)15) + 64; }
+#endif
+
 hipError_t ldpc_prepare(const LdpcGeom& g) {
+#if PL_DIAG
+    if (int f = bp_fpb(g); f > 1)
+        return hipFuncSetAttribute(reg_fpb_kernel(f, g.algo), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)fpb_lds(g, f));
+#endif
     void* k = pick_kernel(g);
     return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds_bytes);
 }
@@ -1008,6 +1061,14 @@ hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, i
     LdpcDev dd = d;
     void* args[] = {&gg, &dd, (void*)&llr, (void*)&ld, (void*)&bits, (void*)&iters, (void*)&batch,
                     (void*)&work};
+#if PL_DIAG
+    if (int f = bp_fpb(g); f > 1) {
+        gg.lds_bytes = (int)(((size_t)g.lds_bytes + 15) & ~(size_t)15);  // per-frame LDS stride
+        void* args7[] = {&gg, &dd, (void*)&llr, (void*)&ld, (void*)&bits, (void*)&iters, (void*)&batch};
+        return hipLaunchKernel(reg_fpb_kernel(f, g.algo), dim3((unsigned)((batch + f - 1) / f)), dim3(256 * f), args7,
+                               fpb_lds(g, f), s);
+    }
+#endif
     return hipLaunchKernel(k, dim3((unsigned)batch), dim3(g.threads), args, g.lds_bytes, s);
 }
 

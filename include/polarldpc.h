@@ -166,6 +166,15 @@ int pl_debug_polar_stamps(pl_plan* plan, const double* llr_dev, int64_t batch, i
 int pl_debug_polar_fpw(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
                        unsigned long long* stamps_dev, int32_t grid, void* stream);
 
+/* Diagnostic build only (the product library returns PL_EUNSUPPORTED): BP
+ * decode of a (504,252)-class LDPC plan on the degree-grouped kernel with
+ * per-phase s_memtime cycle totals added into stamps_dev[4][8] (per wavefront
+ * index of the workgroup = per SIMD): [0] init, [1] early-stop vote, [2] check
+ * pass, [3] its barrier, [4] variable pass, [5] tanh list, [6] closing
+ * barrier, [7] output.  Timing differs from pl_decode; read shares. */
+int pl_debug_ldpc_stamps(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
+                         int32_t* iters_dev, unsigned long long* stamps_dev, void* stream);
+
 /* Test hook, diagnostic build only (the product library returns
  * PL_EUNSUPPORTED): overwrite the device id a plan is bound to, so the
  * wrong-device check can be exercised on a one-GPU machine.  UNSAFE: it turns

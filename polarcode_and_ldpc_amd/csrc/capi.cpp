@@ -123,6 +123,83 @@ static int check_device(const pl_plan* p) {
     return PL_OK;
 }
 
+// the metric evaluation of the list kernel a plan's NaN frames come from (polar_nan.hip)
+static int redo_metric(const pl_plan* p) {
+    if (!p->tree && !p->generic) return pl::kRedoMetricLane;
+    return p->pg.N <= (1 << PL_METRIC_FUSED_NMAX) ? pl::kRedoMetricFused : pl::kRedoMetricLean;
+}
+
+// ldpc_bp_grp_kernel's variable -> thread-slot map (slot q = 256 j + tid;
+// nslots >= n, -1 = empty).  The variable pass stores T'[tpos] (ds_write_b64:
+// lane groups of 16, bank pair tpos mod 16) and reads C'[tpos] (ds_read_b64:
+// lane groups of 32, element (tl + tpos) mod 32) for each of its DV edges; a
+// group's cost is, per edge k, the largest number of its lanes on one bank.
+// Greedy fill (each slot takes the unplaced variable that adds the fewest
+// same-bank lanes to its two groups), then hill climbing over slot swaps
+// (deterministic xorshift, sideways moves kept).  Any map gives the same
+// decoding; only the LDS conflicts change (MI355X_MICROARCH.md, LDS).
+static std::vector<int> ldpc_var_slots(int n, int dv, const std::vector<int32_t>& tp, int tl, int nslots) {
+    std::vector<int> vm(nslots, -1);
+    {
+        std::vector<char> used(n, 0);
+        std::vector<int> wcnt((size_t)dv * 16), rcnt((size_t)dv * 32);
+        const int empty = nslots - n;  // empty slots go to the end of the last groups
+        for (int q = 0; q < nslots - empty; ++q) {
+            if ((q & 15) == 0) std::fill(wcnt.begin(), wcnt.end(), 0);
+            if ((q & 31) == 0) std::fill(rcnt.begin(), rcnt.end(), 0);
+            int best = -1, bc = 1 << 30;
+            for (int v = 0; v < n; ++v) {
+                if (used[v]) continue;
+                int c = 0;
+                for (int k = 0; k < dv; ++k) {
+                    const int t = tp[(size_t)v * dv + k];
+                    c += wcnt[(size_t)k * 16 + t % 16] + rcnt[(size_t)k * 32 + (t + tl) % 32];
+                }
+                if (c < bc) { bc = c; best = v; if (c == 0) break; }
+            }
+            used[best] = 1;
+            vm[q] = best;
+            for (int k = 0; k < dv; ++k) {
+                const int t = tp[(size_t)best * dv + k];
+                ++wcnt[(size_t)k * 16 + t % 16];
+                ++rcnt[(size_t)k * 32 + (t + tl) % 32];
+            }
+        }
+    }
+    auto gcost = [&](int start, int size, int mod, int add) {
+        int c = 0;
+        for (int k = 0; k < dv; ++k) {
+            int cnt[32] = {0}, mx = 0;
+            for (int q = start; q < start + size; ++q) {
+                const int v = vm[q];
+                if (v < 0) continue;
+                const int b = (tp[(size_t)v * dv + k] + add) % mod;
+                mx = std::max(mx, ++cnt[b]);
+            }
+            c += mx;
+        }
+        return c;
+    };
+    auto groups_cost = [&](int a, int b) {
+        const int wa = a & ~15, wb = b & ~15, ra = a & ~31, rb = b & ~31;
+        int c = gcost(wa, 16, 16, 0) + gcost(ra, 32, 32, tl);
+        if (wb != wa) c += gcost(wb, 16, 16, 0);
+        if (rb != ra) c += gcost(rb, 32, 32, tl);
+        return c;
+    };
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    const int iters = 40 * nslots;
+    for (int it = 0; it < iters; ++it) {
+        const int a = (int)(rnd() % (uint64_t)nslots), b = (int)(rnd() % (uint64_t)nslots);
+        if (a == b || (vm[a] < 0 && vm[b] < 0)) continue;
+        const int before = groups_cost(a, b);
+        std::swap(vm[a], vm[b]);
+        if (groups_cost(a, b) > before) std::swap(vm[a], vm[b]);
+    }
+    return vm;
+}
+
 static int device_cus(int dev) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
@@ -234,9 +311,11 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
             p->redo_blocks = (int)std::max<size_t>(1, std::min<size_t>((size_t)p->redo_blocks, cap / p->redo_unit));
             p->lane_grid_max = p->redo_blocks;
         }
-        // the kernel's dynamic-LDS limit is per function: set it for the largest list once
-        if ((e = pl::nan_redo_prepare(pl::kMaxRedoList)) != hipSuccess) {
+        // the redo kernel's dynamic-LDS limit (a per-function attribute) raised to this list's need
+        if ((e = pl::nan_redo_prepare(list_size)) != hipSuccess) {
             pl_plan_destroy(p);
+            if (e == hipErrorInvalidValue)
+                return fail(PL_EUNSUPPORTED, "list_size: the redo kernel's list state exceeds this device's LDS");
             return hipfail(e, "NaN redo kernel prepare");
         }
     }
@@ -333,6 +412,69 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
             g.lds_bytes = (int)((base + pl::ldpc_reg_list_bytes(g.reg_variant) + 15) & ~(size_t)15);
         }
     }
+    // BP on a reg variant: degree-grouped check products (ldpc_bp_grp_kernel).
+    // Slot s holds edges 64 s .. 64 s + 63 (degree-sorted, check-major); D_s =
+    // the largest check degree among them; check c's inputs sit at T' offset
+    // off[c] (even), padded with 1.0 to the largest D_s of the slots holding its
+    // edges.  PL_LDPC_KERNEL=reg keeps ldpc_reg_kernel's per-lane products.
+    std::vector<int32_t> grp_meta, var_tpos;
+    g.grp = 0;
+    g.tl = 0;
+    if (g.reg_variant && algo == PL_LDPC_BP && maxdc <= 15 && !(lk && std::string(lk) == "reg")) {
+        const int slots = 4 * pl::ldpc_reg_ept(g.reg_variant);
+        std::vector<int> dslot(slots, 0), dpad(m, 0), off(m + 1, 0);
+        for (int e = 0; e < E; ++e) {
+            const int c = edge_chk[e], d = row_ptr[c + 1] - row_ptr[c];
+            dslot[e / 64] = std::max(dslot[e / 64], d);
+        }
+        for (int e = 0; e < E; ++e) dpad[edge_chk[e]] = std::max(dpad[edge_chk[e]], dslot[e / 64]);
+        for (int c = 0; c < m; ++c) off[c + 1] = off[c] + ((dpad[c] + 1) & ~1);
+        const int tl = std::max(off[m], 2);
+        const size_t base = ((size_t)16 * tl + (size_t)4 * ((m + 3) & ~3) + 15) & ~(size_t)15;  // T', C', syndrome
+        const size_t lds = (base + pl::ldpc_reg_list_bytes(g.reg_variant) + 15) & ~(size_t)15;
+        if (tl < 65536 && lds <= 64 * 1024) {
+            g.grp = 1;
+            g.tl = tl;
+            g.lds_bytes = (int)lds;
+            // sorted slot s goes to the thread slot (j = s / 4, wavefront w) in snake
+            // order (w = s % 4 for even j, 3 - s % 4 for odd j), so the four
+            // wavefronts -- one per SIMD -- get products of about equal total length
+            grp_meta.assign((size_t)slots * 64, 0);
+            for (int s = 0; s < slots; ++s) {
+                const int j = s / 4, w = (j & 1) ? 3 - (s & 3) : (s & 3);
+                for (int l = 0; l < 64; ++l) {
+                    const int e = 64 * s + l, q = 256 * j + 64 * w + l;
+                    if (e < E) {
+                        const int c = edge_chk[e];
+                        grp_meta[q] = off[c] | ((e - row_ptr[c]) << 16) | (dslot[s] << 20);
+                    } else {  // reads T'[0 .. D_s), skips nothing, stores nothing
+                        grp_meta[q] = (15 << 16) | (dslot[s] << 20);
+                    }
+                }
+            }
+            // variables in thread-slot order (slot q = 256 j + tid): T' position and
+            // check of each edge, variable index (-1: empty); the order chosen so
+            // the variable pass's scattered LDS accesses conflict little
+            std::vector<int32_t> tp((size_t)n * maxdv), vck((size_t)n * maxdv);
+            for (int v = 0; v < n; ++v)
+                for (int k = 0; k < maxdv; ++k) {
+                    const int e = var_edge[var_ptr[v] + k], c = edge_chk[e];
+                    tp[(size_t)v * maxdv + k] = off[c] + (e - row_ptr[c]);
+                    vck[(size_t)v * maxdv + k] = c;
+                }
+            const int nslots = 256 * pl::ldpc_reg_vpt(g.reg_variant);
+            const std::vector<int> vmap = ldpc_var_slots(n, maxdv, tp, tl, nslots);
+            var_tpos.assign((size_t)nslots * (2 * maxdv + 1), 0);
+            for (int q = 0; q < nslots; ++q) {
+                const int v = vmap[q];
+                var_tpos[(size_t)2 * maxdv * nslots + q] = v;
+                for (int k = 0; k < maxdv; ++k) {
+                    var_tpos[(size_t)q * maxdv + k] = v >= 0 ? tp[(size_t)v * maxdv + k] : 0;
+                    var_tpos[(size_t)maxdv * nslots + (size_t)q * maxdv + k] = v >= 0 ? vck[(size_t)v * maxdv + k] : 0;
+                }
+            }
+        }
+    }
     // min-sum codes whose T/C arrays exceed LDS: compressed check state in LDS
     g.compact = 0;
     if (g.use_global && algo == 1 && maxdc <= 15 && !(lk && std::string(lk) == "generic")) {
@@ -366,6 +508,9 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     all.insert(all.end(), edge_meta.begin(), edge_meta.end());
     all.insert(all.end(), var_chk.begin(), var_chk.end());
     all.insert(all.end(), var_cp.begin(), var_cp.end());
+    const size_t grp_at = all.size();
+    all.insert(all.end(), grp_meta.begin(), grp_meta.end());
+    all.insert(all.end(), var_tpos.begin(), var_tpos.end());
     hipError_t e = upload(&p->d_ldpc, all);
     if (e != hipSuccess) { pl_plan_destroy(p); return hipfail(e, "plan upload"); }
     p->ld.row_ptr = p->d_ldpc;
@@ -376,6 +521,8 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     p->ld.edge_meta = p->ld.var_edge + E;
     p->ld.var_chk = p->ld.edge_meta + E;
     p->ld.var_cp = p->ld.var_chk + E;
+    p->ld.grp_meta = g.grp ? p->d_ldpc + grp_at : nullptr;
+    p->ld.var_tpos = g.grp ? p->d_ldpc + grp_at + grp_meta.size() : nullptr;
     if ((e = pl::ldpc_prepare(g)) != hipSuccess) { pl_plan_destroy(p); return hipfail(e, "hipFuncSetAttribute"); }
     p->ws_unit = pl::ldpc_work_bytes_per_frame(g);
     p->ldpc_chunk = std::max(1, env_int("PL_LDPC_CHUNK", 16384));
@@ -420,8 +567,8 @@ static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld,
         if (stamps) return fail(PL_EUNSUPPORTED, "stamps only for the tree kernel");
         // one workgroup per frame, masks = null: every frame
         hipError_t e = pl::nan_redo_launch(llr, ld, bits, batch, p->pg.N, p->pg.K, p->list_size, p->d_frozen_dec,
-                                           p->d_info_pos, p->d_crc_g, nullptr, 0, 1, (unsigned char*)ws, ws_bytes,
-                                           p->redo_blocks, s);
+                                           p->d_info_pos, p->d_crc_g, nullptr, 0, 1, redo_metric(p),
+                                           (unsigned char*)ws, ws_bytes, p->redo_blocks, s);
         return e == hipSuccess ? PL_OK : hipfail(e, "polar generic list launch");
     }
     if (p->kind == 0) {
@@ -454,7 +601,7 @@ static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld,
             if (masks) {
                 // frames whose list saw a NaN metric, in the reference's candidate order
                 e = pl::nan_redo_launch(l0, ld, o0, nb, p->pg.N, p->pg.K, p->list_size, p->d_frozen_dec,
-                                        p->d_info_pos, p->d_crc_g, masks, (int)grid, p->fpw, slices,
+                                        p->d_info_pos, p->d_crc_g, masks, (int)grid, p->fpw, redo_metric(p), slices,
                                         ws_bytes - p->head_bytes, p->redo_blocks, s);
                 if (e != hipSuccess) return hipfail(e, "polar NaN redo launch");
             }
@@ -517,13 +664,16 @@ static int grow_ws(pl_plan* p, Workspace* w, hipStream_t s, size_t need, bool re
                     return hipfail(se, "workspace regrow: stream synchronize");
                 }
             }
+            if (p->mask_bytes) {  // NaN masks start at zero (the decodes keep them so), before the buffer is published
+                hipError_t me = hipMemsetAsync(np, 0, p->mask_bytes, s);
+                if (me != hipSuccess) {
+                    hipFree(np);  // the workspace stays empty: the next decode retries
+                    return hipfail(me, "NaN mask reset");
+                }
+            }
             w->ptr = np;
             w->bytes = want;
             w->failed_need = want < need ? need : 0;
-            if (p->mask_bytes) {  // NaN masks start at zero (the decodes keep them so)
-                hipError_t me = hipMemsetAsync(np, 0, p->mask_bytes, s);
-                if (me != hipSuccess) return hipfail(me, "NaN mask reset");
-            }
             return PL_OK;
         }
         (void)hipGetLastError();  // clear the sticky allocation error before retrying
@@ -645,6 +795,22 @@ extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batc
     std::lock_guard<std::mutex> lk(w->mu);
     if ((rc = grow_ws(p, w.get(), s, ws_need(p, batch), false))) return rc;
     return decode_impl(p, llr, batch, ld, bits, nullptr, w->ptr, w->bytes, stamps_dev, s);
+#endif
+}
+
+extern "C" int pl_debug_ldpc_stamps(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
+                                    int32_t* iters, unsigned long long* stamps_dev, void* stream) {
+    if (!p || p->kind != 1 || !stamps_dev) return fail(PL_EINVAL, "LDPC plan and stamp buffer required");
+#if !PL_DIAG
+    (void)llr; (void)batch; (void)ld; (void)bits; (void)iters; (void)stream;
+    return fail(PL_EUNSUPPORTED, "stamped kernels are in the diagnostic build only (make DIAG=1)");
+#else
+    int rc = check_decode_args(p, batch, ld, llr, bits);
+    if (rc || batch == 0) return rc;
+    if ((rc = check_device(p))) return rc;
+    if (!p->lg.grp || p->lg.reg_variant != 1) return fail(PL_EUNSUPPORTED, "stamps only for the grouped (504,252)-size BP kernel");
+    hipError_t e = pl::ldpc_launch_stamped(p->lg, p->ld, llr, ld, bits, iters, batch, stamps_dev, (hipStream_t)stream);
+    return e == hipSuccess ? PL_OK : hipfail(e, "stamped LDPC launch");
 #endif
 }
 

@@ -3,6 +3,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef PL_METRIC_FUSED_NMAX
+// polar tree instances with n <= this use the fused log1p(exp(-x))
+// (log1p_exp_neg): N=1024 L=8 -1.9 %, L=32 -2.6 %; N=4096 L=8 +3.6 % (register
+// allocation), so larger codes keep log1p_pos(exp_neg(x)) (polar_common.hpp)
+#define PL_METRIC_FUSED_NMAX 10
+#endif
+
 namespace pl {
 
 constexpr int kMaxDepth = 15;  // N <= 2^15
@@ -67,10 +74,14 @@ inline size_t nan_mask_region(int64_t grid) { return ((size_t)grid * 8 * kNanMas
 size_t nan_redo_unit(int N, int list_size);  // scratch bytes per redo workgroup
 int nan_redo_lds_bytes(int list_size);
 hipError_t nan_redo_prepare(int list_size);
+// path-metric evaluation of the list kernel whose frames are redone: the lane
+// kernel's path_metrics (libm-style log1p(exp(-x))), or the tree instances'
+// path_metrics_fast with the fused (n <= PL_METRIC_FUSED_NMAX) or lean form
+enum RedoMetric { kRedoMetricLane = 0, kRedoMetricFused = 1, kRedoMetricLean = 2 };
 hipError_t nan_redo_launch(const double* llr, int64_t ld, uint8_t* out, int64_t batch, int N, int K, int Lsz,
                            const uint32_t* frozen_dec, const int32_t* info_pos, const uint32_t* crc_g,
-                           uint64_t* masks, int grid, int fpw, unsigned char* scratch, size_t scratch_bytes,
-                           int max_blocks, hipStream_t s);
+                           uint64_t* masks, int grid, int fpw, int metric, unsigned char* scratch,
+                           size_t scratch_bytes, int max_blocks, hipStream_t s);
 
 #if PL_DIAG
 // frame-per-wavefront SCL N=1024 L=8 prototype (polar_fpw.hip, diagnostic build)
@@ -107,6 +118,8 @@ struct LdpcGeom {
     int reg_variant;   // > 0: ldpc_reg_kernel instance (constant variable degree, LDS state)
     int compact;       // 1: ldpc_ms_compact_kernel (min-sum, compressed check state in LDS)
     int regular;       // every check has degree maxdc and every variable degree maxdv
+    int grp;           // BP reg variant: ldpc_bp_grp_kernel (degree-grouped products, padded T'/C')
+    int tl;            // grp: length of the padded T'/C' arrays (doubles)
 };
 struct LdpcDev {
     const int32_t* row_ptr;   // [m+1]
@@ -117,12 +130,24 @@ struct LdpcDev {
     const int32_t* edge_meta; // [E]   first edge of the edge's check | check degree << 20
     const int32_t* var_chk;   // [E]   check of var_edge[k]
     const int32_t* var_cp;    // [E]   check << 4 | position in the check, of var_edge[k]
+    // grp (ldpc_bp_grp_kernel): per edge slot (256 EPT of them) the T' position
+    // of the edge's check | position in the check << 16 | its slot's D_s << 20;
+    // per variable slot q (256 VPT of them): [q][DV] T' positions, [q][DV]
+    // checks, then [q] the variable (-1: none)
+    const int32_t* grp_meta;  // [256 EPT]
+    const int32_t* var_tpos;  // [256 VPT (2 DV + 1)]
 };
 hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, int64_t ld,
                        uint8_t* bits, int32_t* iters, int64_t batch, double* work, hipStream_t s);
 hipError_t ldpc_prepare(const LdpcGeom& g);
+#if PL_DIAG
+hipError_t ldpc_launch_stamped(const LdpcGeom& g, const LdpcDev& d, const double* llr, int64_t ld, uint8_t* bits,
+                               int32_t* iters, int64_t batch, unsigned long long* stamps, hipStream_t s);
+#endif
 size_t ldpc_work_bytes_per_frame(const LdpcGeom& g);
 int ldpc_reg_variant(int dv, int E, int n);  // 0: none fits
 size_t ldpc_reg_list_bytes(int variant);      // BP tanh lists of an ldpc_reg_kernel instance
+int ldpc_reg_ept(int variant);                // edges per thread of an ldpc_reg_kernel instance
+int ldpc_reg_vpt(int variant);                // variables per thread
 
 }  // namespace pl

@@ -503,8 +503,251 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
     if (iters && tid == 0) iters[frame] = done;
 }
 
+// ---- BP with degree-grouped check products (ldpc_bp_grp_kernel)
+// The edge slots of ldpc_reg_kernel (slot s = 4 j + wavefront: edges 64 s ..
+// 64 s + 63 of the degree-sorted check-major order) span one or two check
+// degrees each.  The host gives every slot its maximum degree D_s and lays the
+// check inputs out per check, 16-byte aligned and padded with 1.0 up to the
+// largest D_s among the slots holding the check's edges (T'[], C'[] of length
+// tl; the pads are written once and never change).  A lane's product is then
+// the same instruction stream for its whole wavefront: the D_s inputs of its
+// check read as D_s/2 ds_read_b128 at immediate offsets, multiplied left to
+// right with the lane's own factor skipped through the exec mask.  x * 1.0 = x,
+// so every lane gets exactly the sequential product over its check's other
+// inputs (decoder.py:87) -- no per-factor pointer select, no per-lane trip
+// count, one LDS round trip per product.
+
+// p *= t0 (then t1) on the lanes whose position i is not K (resp. K + 1): the
+// compare, the exec mask and the multiplies in one block (the compare kept
+// inside, so it is not hoisted out of the iteration loop into SGPRs)
+template <int K>
+PL_DEV double mul_skip1(double p, double t0, int i) {
+    uint64_t sv, m0;
+    asm("v_cmp_ne_u32_e64 %[m0], %[k0], %[i]\n\t"
+        "s_and_saveexec_b64 %[sv], %[m0]\n\t"
+        "v_mul_f64 %[p], %[p], %[t0]\n\t"
+        "s_mov_b64 exec, %[sv]"
+        : [p] "+v"(p), [sv] "=&s"(sv), [m0] "=&s"(m0)
+        : [k0] "n"(K), [i] "v"(i), [t0] "v"(t0)
+        : "scc");
+    return p;
+}
+template <int K>
+PL_DEV double mul_skip2(double p, double2 t, int i) {
+    uint64_t sv, m0, m1;
+    asm("v_cmp_ne_u32_e64 %[m0], %[k0], %[i]\n\t"
+        "v_cmp_ne_u32_e64 %[m1], %[k1], %[i]\n\t"
+        "s_and_saveexec_b64 %[sv], %[m0]\n\t"
+        "v_mul_f64 %[p], %[p], %[t0]\n\t"
+        "s_and_b64 exec, %[sv], %[m1]\n\t"
+        "v_mul_f64 %[p], %[p], %[t1]\n\t"
+        "s_mov_b64 exec, %[sv]"
+        : [p] "+v"(p), [sv] "=&s"(sv), [m0] "=&s"(m0), [m1] "=&s"(m1)
+        : [k0] "n"(K), [k1] "n"(K + 1), [i] "v"(i), [t0] "v"(t.x), [t1] "v"(t.y)
+        : "scc");
+    return p;
+}
+template <int Q, int D>
+PL_DEV double grp_mul_pairs(double p, const double2* t, int i) {
+    if constexpr (2 * Q + 1 < D) return grp_mul_pairs<Q + 1, D>(mul_skip2<2 * Q>(p, t[Q], i), t, i);
+    else if constexpr (2 * Q + 1 == D) return mul_skip1<2 * Q>(p, t[Q].x, i);
+    else return p;
+}
+// the product over positions k < D, k != i, of the check inputs at tb
+template <int D>
+PL_DEV double grp_prod(const double* tb, int i) {
+    const double2* t2 = reinterpret_cast<const double2*>(tb);
+    double2 t[(D + 1) / 2];
+#pragma unroll
+    for (int q = 0; q < (D + 1) / 2; ++q) t[q] = t2[q];
+    return grp_mul_pairs<0, D>(1.0, t, i);
+}
+
+// STAMPS (diagnostic build): per-phase s_memtime cycles of every wavefront,
+// summed into stamps[wavefront][8] (init, vote, check pass, its barrier,
+// variable pass, tanh list, closing barrier, output).
+template <int DV, int EPT, int VPT, bool STAMPS = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
+                   uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch,
+                   unsigned long long* __restrict__ stamps) {
+    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tprev = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+#define PL_GSTAMP(k)                                               \
+    if constexpr (STAMPS) {                                        \
+        const unsigned long long tn = __builtin_amdgcn_s_memtime(); \
+        st[k] += tn - tprev;                                       \
+        tprev = tn;                                                \
+    }
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int NT = 256;
+    const int64_t frame = blockIdx.x;
+    if (frame >= batch) return;
+    const int tid = threadIdx.x;
+    const int n = g.n, m = g.m, tl = g.tl;
+    double* T = reinterpret_cast<double*>(smem);  // T'[tl]: check inputs, per check, padded
+    double* C = T + tl;                           // C'[tl]: check-to-variable, same positions
+    // syndrome of the current decisions, kept across iterations: a variable
+    // whose decision flips toggles its checks' parities (no per-iteration reset,
+    // and the LDS atomics only where a decision changed)
+    const int mp = (m + 3) & ~3;
+    uint32_t* syn = reinterpret_cast<uint32_t*>(smem + (size_t)16 * tl);  // [mp]
+    uint16_t* work = reinterpret_cast<uint16_t*>(smem + (((size_t)16 * tl + (size_t)4 * mp + 15) & ~(size_t)15));
+    const double* __restrict__ ch = llr + frame * ld;
+    const int lane = __lane_id();
+
+    int meta[EPT];  // T' position of the edge's check | position in the check << 16 | D_s << 20
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        const int e = tid + j * NT;
+        meta[j] = dv.grp_meta[e];  // [256 EPT], host-assigned edges (position 15: none)
+    }
+    // variables by thread slot q = tid + 256 j (host-chosen order):
+    // var_tpos = [T' positions of the slot's DV edges][their checks][variable or -1]
+    int ve[VPT][DV], vc[VPT][DV], vid[VPT];
+    double chv[VPT];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+        const int q = tid + j * NT;
+        vid[j] = dv.var_tpos[2 * DV * NT * VPT + q];
+        const bool ok = vid[j] >= 0;
+#pragma unroll
+        for (int k = 0; k < DV; ++k) {
+            ve[j][k] = dv.var_tpos[q * DV + k];
+            vc[j][k] = dv.var_tpos[DV * NT * VPT + q * DV + k];
+        }
+        chv[j] = ok ? ch[vid[j]] : 0.0;
+    }
+    for (int c = tid; c < mp; c += NT) syn[c] = 0u;  // H * 0
+    uint32_t decs = 0;  // bit j: the decision of variable tid + 256 j (initially 0)
+    for (int q = tid; q < tl; q += NT) T[q] = 1.0;  // the pads
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+        if (vid[j] >= 0) {
+            const double t = tanh_half_clip(chv[j]);
+#pragma unroll
+            for (int k = 0; k < DV; ++k) {
+                T[ve[j][k]] = t;
+                C[ve[j][k]] = 0.0;
+            }
+        }
+    }
+    __syncthreads();
+    PL_GSTAMP(0)
+    int done = g.max_iter;
+    for (int it = 0; it < g.max_iter; ++it) {
+#ifndef PL_ABL_VOTE
+        if (g.early_stop && it > 0) {
+            // every wavefront reads all m parities itself (the previous closing
+            // barrier made them complete) and reaches the same verdict: no
+            // cross-wavefront vote, no barrier (__syncthreads_or costs three)
+            uint32_t bad = 0;
+            for (int c = 4 * lane; c < m; c += 256) {
+                if (c + 4 <= m) {
+                    const uint4 w4 = *reinterpret_cast<const uint4*>(syn + c);
+                    bad |= w4.x | w4.y | w4.z | w4.w;
+                } else {
+                    for (int k = c; k < m; ++k) bad |= syn[k];
+                }
+            }
+            if (!__ballot(bad != 0u)) { done = it; break; }
+        }
+#endif
+        PL_GSTAMP(1)
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int D = __builtin_amdgcn_readfirstlane(meta[j] >> 20);  // the slot's D_s
+            if (D == 0) continue;                                          // slot past the last edge
+            const int base = meta[j] & 0xFFFF, i = (meta[j] >> 16) & 15;
+            const double* tb = T + base;
+            double p;
+            switch (D) {
+                case 1: p = grp_prod<1>(tb, i); break;
+                case 2: p = grp_prod<2>(tb, i); break;
+                case 3: p = grp_prod<3>(tb, i); break;
+                case 4: p = grp_prod<4>(tb, i); break;
+                case 5: p = grp_prod<5>(tb, i); break;
+                case 6: p = grp_prod<6>(tb, i); break;
+                case 7: p = grp_prod<7>(tb, i); break;
+                case 8: p = grp_prod<8>(tb, i); break;
+                case 9: p = grp_prod<9>(tb, i); break;
+                case 10: p = grp_prod<10>(tb, i); break;
+                case 11: p = grp_prod<11>(tb, i); break;
+                case 12: p = grp_prod<12>(tb, i); break;
+                case 13: p = grp_prod<13>(tb, i); break;
+                case 14: p = grp_prod<14>(tb, i); break;
+                default: p = grp_prod<15>(tb, i); break;
+            }
+            // clip, 2*atanh, nan_to_num: after the clip 2*atanh is finite, so
+            // only a NaN product (NaN channel LLRs) maps to 0
+            const bool pn = __builtin_isnan(p);
+            double o = two_atanh(__builtin_fmax(__builtin_fmin(p, 0.999999), -0.999999));
+            o = pn ? 0.0 : o;
+            if (i != 15) C[base + i] = o;  // 15: no edge in this lane of the slot
+        }
+        PL_GSTAMP(2)
+        __syncthreads();
+        PL_GSTAMP(3)
+        uint16_t* const wl = work + (tid >> 6) * (64 * VPT * DV);  // this wavefront's tanh list
+        int wn = 0;
+#pragma unroll
+        for (int j = 0; j < VPT; ++j) {
+            const bool vok = vid[j] >= 0;
+            if (!__ballot(vok)) continue;
+            double c2v[DV];
+            double sum = 0.0;  // np.sum over DV < 8 messages: sequential
+#pragma unroll
+            for (int k = 0; k < DV; ++k) {
+                c2v[k] = C[ve[j][k]];
+                sum += c2v[k];
+            }
+            const double total = chv[j] + sum;
+            const bool one = total <= 0.0;
+            const bool flip = vok && (one != (((decs >> j) & 1u) != 0u));
+            decs ^= flip ? (1u << j) : 0u;
+#pragma unroll
+            for (int k = 0; k < DV; ++k) {
+                const double x = total - c2v[k];  // v2c as decoder.py:120 forms it
+                const bool sat = fabs(x) > 14.52;
+                if (vok) T[ve[j][k]] = sat ? __builtin_copysign(0.999999, x) : x;
+                const bool need = vok && !sat;
+                const uint64_t nb = __ballot(need);
+                const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nb >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)nb, 0u));
+                if (need) wl[wn + pre] = (uint16_t)ve[j][k];
+                wn += (int)__popcll(nb);
+#ifndef PL_ABL_SYN
+                if (flip) atomicXor(&syn[vc[j][k]], 1u);
+#endif
+            }
+        }
+        PL_GSTAMP(4)
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (int w = lane; w < wn; w += 64) {
+            const int e = wl[w];
+            T[e] = tanh_half_clip(T[e]);
+        }
+        PL_GSTAMP(5)
+        __syncthreads();
+        PL_GSTAMP(6)
+    }
+    uint8_t* o = bits + frame * (int64_t)n;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j)
+        if (vid[j] >= 0) o[vid[j]] = (uint8_t)((decs >> j) & 1u);
+    if (iters && tid == 0) iters[frame] = done;
+    PL_GSTAMP(7)
+    if constexpr (STAMPS) {
+        if (lane == 0)
+            for (int k = 0; k < 8; ++k) atomicAdd(&stamps[(tid >> 6) * 8 + k], st[k]);
+    }
+#undef PL_GSTAMP
+}
+
 // (DV, EPT, VPT) instances of ldpc_reg_kernel: E <= 256*EPT, n <= 256*VPT
-struct RegVariant { int dv, ept, vpt; void* k[2]; };
+struct RegVariant { int dv, ept, vpt; void* k[3]; };  // BP, MS, BP degree-grouped
 #if PL_DIAG
 static void* reg_fpb_kernel(int fpb, int algo) {  // diagnostic FPB instances of the (3, 6, 2) variant
     if (fpb == 2) return algo == 0 ? (void*)ldpc_reg_kernel<0, 3, 6, 2, 2> : (void*)ldpc_reg_kernel<1, 3, 6, 2, 2>;
@@ -514,7 +757,9 @@ static void* reg_fpb_kernel(int fpb, int algo) {  // diagnostic FPB instances of
 #endif
 template <int DV, int EPT, int VPT>
 static RegVariant reg_variant() {
-    return {DV, EPT, VPT, {(void*)ldpc_reg_kernel<0, DV, EPT, VPT>, (void*)ldpc_reg_kernel<1, DV, EPT, VPT>}};
+    return {DV, EPT, VPT,
+            {(void*)ldpc_reg_kernel<0, DV, EPT, VPT>, (void*)ldpc_reg_kernel<1, DV, EPT, VPT>,
+             (void*)ldpc_bp_grp_kernel<DV, EPT, VPT>}};
 }
 static const RegVariant* reg_table(int& count) {
     static const RegVariant t[] = {reg_variant<3, 6, 2>(), reg_variant<3, 8, 2>(), reg_variant<3, 12, 4>(),
@@ -526,6 +771,16 @@ size_t ldpc_reg_list_bytes(int variant) {
     int cnt;
     const RegVariant* t = reg_table(cnt);
     return variant > 0 && variant <= cnt ? (size_t)256 * t[variant - 1].vpt * t[variant - 1].dv * 2 : 0;
+}
+int ldpc_reg_vpt(int variant) {
+    int cnt;
+    const RegVariant* t = reg_table(cnt);
+    return variant > 0 && variant <= cnt ? t[variant - 1].vpt : 0;
+}
+int ldpc_reg_ept(int variant) {
+    int cnt;
+    const RegVariant* t = reg_table(cnt);
+    return variant > 0 && variant <= cnt ? t[variant - 1].ept : 0;
 }
 int ldpc_reg_variant(int dv, int E, int n) {
     int cnt;
@@ -724,6 +979,16 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
     int done = g.max_iter;
     for (int it = 0; it < g.max_iter; ++it) {
         int syn = 0;
+        if constexpr (RI) {
+            // opaque to the compiler each iteration: the packed indices stay packed
+            // (hoisted out of the loop as 24 unpacked LDS addresses they pushed the
+            // kernel to 44 B of scratch per lane, whose stores reached HBM: +2.9 GB
+            // per launch at n = 8192)
+#pragma unroll
+            for (int q = 0; q < MQ; ++q)
+#pragma unroll
+                for (int k = 0; k < DC / 2; ++k) asm volatile("" : "+v"(ccol[q][k]));
+        }
         if constexpr (RI && DV > 0 && DV < 8 && PL_MS_CB > 0) {
             // regular code, indices in registers: the loads of PL_MS_CB checks
             // (their old state and DC totals) issue before any of them is
@@ -1028,7 +1293,7 @@ static void* pick_kernel(const LdpcGeom& g) {
     }
     if (g.reg_variant) {
         int cnt;
-        return reg_table(cnt)[g.reg_variant - 1].k[g.algo == 0 ? 0 : 1];
+        return reg_table(cnt)[g.reg_variant - 1].k[g.algo != 0 ? 1 : (g.grp ? 2 : 0)];
     }
 #if PL_DIAG
     if (g.check_kernel) return g.algo == 0 ? (void*)ldpc_check_kernel<0> : (void*)ldpc_check_kernel<1>;
@@ -1042,6 +1307,21 @@ static int bp_fpb(const LdpcGeom& g) {  // PL_BP_FPB=2|4: the reg (3, 6, 2) vari
     return (v == 2 || v == 4) && g.reg_variant == 1 ? v : 1;
 }
 static size_t fpb_lds(const LdpcGeom& g, int f) { return (size_t)f * (((size_t)g.lds_bytes + 15) & ~(size_t)15) + 64; }
+#endif
+
+#if PL_DIAG
+// the degree-grouped BP kernel of a grp plan with per-phase stamps (4 x 8 u64)
+hipError_t ldpc_launch_stamped(const LdpcGeom& g, const LdpcDev& d, const double* llr, int64_t ld, uint8_t* bits,
+                               int32_t* iters, int64_t batch, unsigned long long* stamps, hipStream_t s) {
+    if (!g.grp || g.reg_variant != 1) return hipErrorInvalidValue;
+    void* k = (void*)ldpc_bp_grp_kernel<3, 6, 2, true>;
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds_bytes);
+    if (e != hipSuccess) return e;
+    LdpcGeom gg = g;
+    LdpcDev dd = d;
+    void* args[] = {&gg, &dd, (void*)&llr, (void*)&ld, (void*)&bits, (void*)&iters, (void*)&batch, (void*)&stamps};
+    return hipLaunchKernel(k, dim3((unsigned)batch), dim3(256), args, g.lds_bytes, s);
+}
 #endif
 
 hipError_t ldpc_prepare(const LdpcGeom& g) {

@@ -6,13 +6,7 @@
 #pragma once
 #include "common.hpp"
 #include "fp64_math.hpp"
-
-#ifndef PL_METRIC_FUSED_NMAX
-// tree instances with n <= this use the fused log1p(exp(-x)) (log1p_exp_neg):
-// N=1024 L=8 -1.9 %, L=32 -2.6 %; N=4096 L=8 +3.6 % (register allocation), so
-// larger codes keep log1p_pos(exp_neg(x)); bits identical on every polar GPU test
-#define PL_METRIC_FUSED_NMAX 10
-#endif
+#include "internal.hpp"  // PL_METRIC_FUSED_NMAX
 
 namespace pl {
 

@@ -13,7 +13,10 @@
 // state in global scratch, thread 0 running CPython's sort (pysort.hpp) on the
 // candidates, survivors renumbered in that order, argmax = first NaN else first
 // maximum.  f, g and the metric increments are the list kernels' own
-// (polar_common.hpp), so on finite values this decodes exactly as they do.
+// (polar_common.hpp), each frame with the metric evaluation of the kernel that
+// flagged it (RedoArgs::metric: the lane kernel's libm-style log1p(exp(-x)),
+// or the tree instance's fused / lean one), so on finite values a flagged frame
+// decodes exactly as that kernel decodes it.
 //
 // Scratch per workgroup (nan_redo_unit): for each of the L physical path
 // buffers, the LLR arrays of depths 1..n (N - 1 doubles: depth d at offset
@@ -27,6 +30,7 @@
 // paths (up to kMaxRedoList; the list kernels hold one lane per path in one
 // workgroup): every frame, one workgroup each.
 #include <algorithm>
+#include <mutex>
 
 #include "common.hpp"
 #include "internal.hpp"
@@ -50,6 +54,7 @@ struct RedoArgs {
     const uint32_t* crc_g;   // CA-SCL table, or null
     uint64_t* masks;         // [grid][kNanMaskPasses]: bit f of word p = frame f of pass p flagged
     int grid, fpw;           // the list kernel's grid and frames per wavefront
+    int metric;              // RedoMetric of the kernel whose frames these are
     unsigned char* scratch;  // nan_redo_unit bytes per redo workgroup
     size_t unit;
 };
@@ -92,7 +97,6 @@ PL_DEV void redo_frame(const RedoArgs& a, int64_t frame, const Bufs& bf, unsigne
     int* flag = nbit + L;                                          // [L] claimed / used scratch
     int* shared = flag + L;                                        // [4]
     const double* ch = a.llr + frame * a.ld;
-    const bool fused = n <= PL_METRIC_FUSED_NMAX;  // the metric evaluation of the tree instances it stands in for
 
     for (int p = tid; p < L; p += kRedoThreads) {
         phys[p] = p;
@@ -123,8 +127,9 @@ PL_DEV void redo_frame(const RedoArgs& a, int64_t frame, const Bufs& bf, unsigne
             for (int p = tid; p < nact; p += kRedoThreads) {
                 const double lam = bf.llr(phys[p])[dep_off(N, n)];
                 double m0, m1;
-                if (fused) path_metrics_fast<false, true>(pm[p], lam, true, m0, m1);
-                else path_metrics_fast<false, false>(pm[p], lam, true, m0, m1);
+                if (a.metric == kRedoMetricFused) path_metrics_fast<false, true>(pm[p], lam, true, m0, m1);
+                else if (a.metric == kRedoMetricLean) path_metrics_fast<false, false>(pm[p], lam, true, m0, m1);
+                else path_metrics<false>(pm[p], lam, m0, m1);
                 pm[p] = m0;
                 nbit[p] = 0;
             }
@@ -133,8 +138,9 @@ PL_DEV void redo_frame(const RedoArgs& a, int64_t frame, const Bufs& bf, unsigne
             for (int p = tid; p < nact; p += kRedoThreads) {
                 const double lam = bf.llr(phys[p])[dep_off(N, n)];
                 double m0, m1;
-                if (fused) path_metrics_fast<true, true>(pm[p], lam, true, m0, m1);
-                else path_metrics_fast<true, false>(pm[p], lam, true, m0, m1);
+                if (a.metric == kRedoMetricFused) path_metrics_fast<true, true>(pm[p], lam, true, m0, m1);
+                else if (a.metric == kRedoMetricLean) path_metrics_fast<true, false>(pm[p], lam, true, m0, m1);
+                else path_metrics<true>(pm[p], lam, m0, m1);
                 cand[p] = PsItem{m0, p, 0};             // path_metrics_0 (decoder.py:300-303)
                 cand[nact + p] = PsItem{m1, nact + p, 0};  // path_metrics_1, after every bit-0 candidate
             }
@@ -317,18 +323,32 @@ size_t nan_redo_unit(int N, int list_size) { return path_bytes(N) * (size_t)list
 
 int nan_redo_lds_bytes(int list_size) { return (int)(lds_frame_bytes(list_size) + 16 * kRedoThreads + 16); }
 
+// The kernel's dynamic-LDS limit is a per-function attribute: raise it to what
+// this plan's list needs (never lower it under another plan), per device.
 hipError_t nan_redo_prepare(int list_size) {
-    return hipFuncSetAttribute((const void*)polar_nan_redo_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               nan_redo_lds_bytes(list_size));
+    static std::mutex mu;
+    static int set_bytes[64] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const int need = nan_redo_lds_bytes(list_size);
+    std::lock_guard<std::mutex> lk(mu);
+    if (dev >= 0 && dev < 64 && need <= set_bytes[dev]) return hipSuccess;
+    int optin = 0;
+    if ((e = hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev)) != hipSuccess) return e;
+    if (need > optin) return hipErrorInvalidValue;  // this list's state does not fit the device's LDS
+    e = hipFuncSetAttribute((const void*)polar_nan_redo_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, need);
+    if (e == hipSuccess && dev >= 0 && dev < 64) set_bytes[dev] = need;
+    return e;
 }
 
 hipError_t nan_redo_launch(const double* llr, int64_t ld, uint8_t* out, int64_t batch, int N, int K, int Lsz,
                            const uint32_t* frozen_dec, const int32_t* info_pos, const uint32_t* crc_g,
-                           uint64_t* masks, int grid, int fpw, unsigned char* scratch, size_t scratch_bytes,
-                           int max_blocks, hipStream_t s) {
+                           uint64_t* masks, int grid, int fpw, int metric, unsigned char* scratch,
+                           size_t scratch_bytes, int max_blocks, hipStream_t s) {
     int n = 0;
     while ((1 << n) < N) ++n;
-    RedoArgs a{llr, ld, out, batch, N, n, K, Lsz, frozen_dec, info_pos, crc_g, masks, grid, fpw, scratch,
+    RedoArgs a{llr, ld, out, batch, N, n, K, Lsz, frozen_dec, info_pos, crc_g, masks, grid, fpw, metric, scratch,
                nan_redo_unit(N, Lsz)};
     const int64_t fit = (int64_t)(scratch_bytes / a.unit);
     // masks: one workgroup per list-kernel wavefront at most; no masks: per frame

@@ -44,3 +44,15 @@ def test_bench_self_launch_two_ranks():
 def test_bench_single_rank_counts():
     r = _run(1, 96, 2)
     assert r["n_gpus"] == 1 and r["counts"] == _expected(1, 96, 2)
+
+
+def test_bench_self_launch_eight_ranks():
+    """The driver's N=8 shape end to end on CPU: self-launch -> torch.distributed.run
+    -> 8 gloo ranks, each timing its own shard; counters all-reduced over the
+    global frame range, one max-over-ranks step time, one time per rank."""
+    r = _run(8, 32, 2)
+    assert r["n_gpus"] == 8 and r["stub"] is True and r["steps"] == 2
+    assert len(r["rank_ms_per_step"]) == 8
+    assert r["ms_per_step"] == max(r["rank_ms_per_step"])
+    assert r["counts"] == _expected(8, 32, 2)
+    assert r["value"] > 0

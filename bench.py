@@ -221,7 +221,18 @@ def cpu_share():
         pass
     cap = int(os.environ.get("PL_BENCH_CPU_CAP", "16"))
     used = max(1, min(aff, quota or aff, cap))
-    return used, dict(host_cpus_affinity=aff, cgroup_cpu_quota=quota, cap=cap, os_cpu_count=os.cpu_count())
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    # cpu_model: the restatement runs within 7 % of the reference on one core of
+    # the same machine (tools/cpu_calibration.py, profiles/r05/cpu_calibration*.json)
+    return used, dict(host_cpus_affinity=aff, cgroup_cpu_quota=quota, cap=cap, os_cpu_count=os.cpu_count(),
+                      cpu_model=model)
 
 
 def cpu_processes():

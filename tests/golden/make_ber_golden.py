@@ -59,6 +59,10 @@ POINTS = {
     "ms20_m10": ("ms", dict(n=8192, dv=3, dc=6, hseed=11, max_iter=20), -1.0, 500000),
     "bp20_m10": ("bp", dict(n=504, k=252, hseed=42, max_iter=20), -1.0, 510000),
     "bp20_p05": ("bp", dict(n=504, k=252, hseed=42, max_iter=20), 0.5, 520000),
+    # round 5: CA-SCL L=32 + CRC-8 at the low end of the
+    # configs[3] sweep; seeds fixed before any GPU run of the test that reads them
+    "cascl32_m20": ("cascl", dict(N=1024, K=512, L=32, crc="CRC-8"), -2.0, 530000),
+    "cascl32_m15": ("cascl", dict(N=1024, K=512, L=32, crc="CRC-8"), -1.5, 540000),
 }
 
 
@@ -93,7 +97,26 @@ def _chunk(task):
     np.random.seed(seed + c)
     ch = channel.AWGNChannel(snr_db=snr, seed=None)
     nf = FRAMES_PER_CHUNK
-    if kind in ("sc", "scl"):
+    if kind == "cascl":
+        # the reference's encoder with use_crc (src/polar/encoder.py:63-87: K - crc
+        # data bits, crc_encode appends the CRC); no reference CA-SCL decoder exists
+        # (decoder.py:202-203,259 store use_crc and never read it), so the frames
+        # are decoded by the oracle's restatement of the build-defined CA-SCL
+        # (oracle.cascl_decode, pinned frame by frame against the GPU kernel)
+        from polarcode_and_ldpc_amd.polar import construct_frozen_set
+        from polar.utils import crc_encode
+        N, K, crc = p["N"], p["K"], p["crc"]
+        fr = construct_frozen_set(N, K, 2.0)
+        enc = polar.PolarEncoder(N, K, frozen_bits=fr, use_crc=True, crc_polynomial=crc)
+        msgs, llrs = [], []
+        for _ in range(nf):
+            m = np.random.randint(0, 2, enc.K_data)
+            msgs.append(crc_encode(m, crc))
+            llrs.append(ch.transmit(enc.encode(m), return_llr=True))
+        msgs, llrs = np.array(msgs), np.array(llrs)
+        dec = oracle.cascl_decode(N, p["L"], fr, llrs, crc_polynomial=crc, threads=1)
+        err = (dec != msgs).sum(axis=1)
+    elif kind in ("sc", "scl"):
         from polarcode_and_ldpc_amd.polar import construct_frozen_set
         N, K = p["N"], p["K"]
         fr = construct_frozen_set(N, K, 2.0)  # ber_simulation.py:146-148 (PolarLibWrapper substitute)
@@ -137,7 +160,7 @@ def main():
     out_path = os.path.join(HERE, "ber_points.npz")
     out = dict(np.load(out_path)) if os.path.exists(out_path) else {}
     # the slow points first so the pool drains evenly
-    order = {"bp": 0, "scl": 1, "sc": 2, "ms": 3}
+    order = {"bp": 0, "cascl": 1, "scl": 1, "sc": 2, "ms": 3}
     tasks = sorted([(n, c) for n in names for c in range(CHUNKS)], key=lambda t: (order[POINTS[t[0]][0]], t))
     got = {n: [None] * CHUNKS for n in names}
     t0 = time.time()

@@ -174,3 +174,24 @@ def test_awgn_llr_moments_and_tails(gpu):
     cw = torch.ones((B, n), dtype=torch.uint8, device="cuda")
     neg = ch.llr_batch_device(cw, n, B, seed=77)
     assert torch.allclose(neg - (llr - 4.0 / s2), torch.zeros_like(neg), atol=1e-9 * (4.0 / s2))
+
+
+@pytest.mark.parametrize("snr,name", [(-2.0, "cascl32_m20"), (-1.5, "cascl32_m15")])
+def test_cascl_l32_crc8_ber_fer_parity(gpu, snr, name):
+    """CA-SCL L=32 + CRC-8 N=1024 K=512 (configs[3] itself) at the low end of its
+    sweep.  Device: harness.montecarlo.polar_round_fn with crc_polynomial
+    (Philox data bits + pl_crc_append, device encoder, AWGN, CASCLDecoder,
+    errors over all K bits as the reference encoder's message_with_crc).
+    Reference side: the reference's PolarEncoder(use_crc=True) frame loop,
+    decoded by the oracle's CA-SCL restatement (the reference has no CA-SCL
+    decoder: decoder.py:202-203,259); 16 384 frames per point, seeds fixed in
+    make_ber_golden.py before any GPU run of this test."""
+    from polarcode_and_ldpc_amd.harness.montecarlo import MonteCarlo, polar_round_fn
+    from polarcode_and_ldpc_amd.polar import CASCLDecoder, construct_frozen_set
+    N, K, L = 1024, 512, 32
+    fr = construct_frozen_set(N, K, 2.0)
+    dec = CASCLDecoder(N, K, L, frozen_bits=fr, crc_polynomial="CRC-8")
+    dev = MonteCarlo(polar_round_fn(dec, seed=106, crc_polynomial="CRC-8"), info_bits=K,
+                     batch=32768).run([snr], 65536, 10 ** 12)[0]
+    r = _compare(dev, _ref_point(name, "cascl", snr), K, "CA-SCL L=32 CRC-8 N=1024 @ %g dB" % snr)
+    assert r["fer_ref"] > 0.005

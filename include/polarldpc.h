@@ -166,6 +166,16 @@ int pl_debug_polar_stamps(pl_plan* plan, const double* llr_dev, int64_t batch, i
 int pl_debug_polar_fpw(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
                        unsigned long long* stamps_dev, int32_t grid, void* stream);
 
+/* Diagnostic build only (the product library returns PL_EUNSUPPORTED): the
+ * dead-store bound of the SCL N=1024 L=8 tree kernel.  mode 1
+ * decodes recording, per frame group of 8 frames, which workspace pool arrays
+ * (depths F..DL-1, one bit per node and lane plane) a right child's g reads and
+ * which were stored: mask_dev u32 [ceil(batch/8)][2][words], zeroed by the
+ * caller; mode 2 decodes the same frames again with every store of an array
+ * not read in mode 1 skipped.  Bits equal pl_decode's by construction. */
+int pl_debug_polar_deadstore(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
+                             uint32_t* mask_dev, int32_t mode, void* stream);
+
 /* Diagnostic build only (the product library returns PL_EUNSUPPORTED): BP
  * decode of a (504,252)-class LDPC plan on the degree-grouped kernel with
  * per-phase s_memtime cycle totals added into stamps_dev[4][8] (per wavefront

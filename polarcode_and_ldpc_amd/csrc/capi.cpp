@@ -429,7 +429,9 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
         }
         for (int e = 0; e < E; ++e) dpad[edge_chk[e]] = std::max(dpad[edge_chk[e]], dslot[e / 64]);
         for (int c = 0; c < m; ++c) off[c + 1] = off[c] + ((dpad[c] + 1) & ~1);
-        const int tl = std::max(off[m], 2);
+        // T', C' positions [0, off[m]) hold the checks, [off[m], off[m] + 16) is a sink
+        // for the lanes of a slot past the last edge (they read it and store into it)
+        const int sink = off[m], tl = off[m] + 16;
         const size_t base = ((size_t)16 * tl + (size_t)4 * ((m + 3) & ~3) + 15) & ~(size_t)15;  // T', C', syndrome
         const size_t lds = (base + pl::ldpc_reg_list_bytes(g.reg_variant) + 15) & ~(size_t)15;
         if (tl < 65536 && lds <= 64 * 1024) {
@@ -447,8 +449,8 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
                     if (e < E) {
                         const int c = edge_chk[e];
                         grp_meta[q] = off[c] | ((e - row_ptr[c]) << 16) | (dslot[s] << 20);
-                    } else {  // reads T'[0 .. D_s), skips nothing, stores nothing
-                        grp_meta[q] = (15 << 16) | (dslot[s] << 20);
+                    } else {  // reads and stores the sink (position 15 skips no factor)
+                        grp_meta[q] = sink | (15 << 16) | (dslot[s] << 20);
                     }
                 }
             }
@@ -464,6 +466,14 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
                 }
             const int nslots = 256 * pl::ldpc_reg_vpt(g.reg_variant);
             const std::vector<int> vmap = ldpc_var_slots(n, maxdv, tp, tl, nslots);
+            // + the pad positions (T' = 1.0 from the first write on), -1 filled to 256
+            std::vector<char> real(sink, 0);
+            for (int e = 0; e < E; ++e) real[off[edge_chk[e]] + (e - row_ptr[edge_chk[e]])] = 1;
+            std::vector<int32_t> pads;
+            for (int q = 0; q < sink; ++q)
+                if (!real[q]) pads.push_back(q);
+            g.npad = (int)((pads.size() + 255) / 256 * 256);
+            pads.resize(g.npad, -1);
             var_tpos.assign((size_t)nslots * (2 * maxdv + 1), 0);
             for (int q = 0; q < nslots; ++q) {
                 const int v = vmap[q];
@@ -473,6 +483,7 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
                     var_tpos[(size_t)maxdv * nslots + (size_t)q * maxdv + k] = v >= 0 ? vck[(size_t)v * maxdv + k] : 0;
                 }
             }
+            var_tpos.insert(var_tpos.end(), pads.begin(), pads.end());
         }
     }
     // min-sum codes whose T/C arrays exceed LDS: compressed check state in LDS
@@ -795,6 +806,28 @@ extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batc
     std::lock_guard<std::mutex> lk(w->mu);
     if ((rc = grow_ws(p, w.get(), s, ws_need(p, batch), false))) return rc;
     return decode_impl(p, llr, batch, ld, bits, nullptr, w->ptr, w->bytes, stamps_dev, s);
+#endif
+}
+
+extern "C" int pl_debug_polar_deadstore(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
+                                        uint32_t* mask_dev, int32_t mode, void* stream) {
+    if (!p || p->kind != 0 || !mask_dev || (mode != 1 && mode != 2)) return fail(PL_EINVAL, "polar plan, mask, mode 1|2");
+#if !PL_DIAG
+    (void)llr; (void)batch; (void)ld; (void)bits; (void)stream;
+    return fail(PL_EUNSUPPORTED, "dead-store instances are in the diagnostic build only (make DIAG=1)");
+#else
+    int rc = check_decode_args(p, batch, ld, llr, bits);
+    if (rc || batch == 0) return rc;
+    if ((rc = check_device(p))) return rc;
+    if (!p->tree || !p->tinfo.fn_ds[0]) return fail(PL_EUNSUPPORTED, "dead-store instances: N=1024 L=8 tree plans only");
+    const hipStream_t s = (hipStream_t)stream;
+    std::shared_ptr<Workspace> w = stream_entry(p, s);
+    std::lock_guard<std::mutex> lk(w->mu);
+    if ((rc = grow_ws(p, w.get(), s, ws_need(p, batch), false))) return rc;
+    pl::g_tree_ds_mode = mode;
+    rc = decode_impl(p, llr, batch, ld, bits, nullptr, w->ptr, w->bytes, reinterpret_cast<unsigned long long*>(mask_dev), s);
+    pl::g_tree_ds_mode = 0;
+    return rc;
 #endif
 }
 

@@ -31,13 +31,15 @@ PL_DEV double fma_k(double a, double b, double c) {
         return fma(a, b, c);
     }
 }
-// x / y to <= 1 ulp: hardware reciprocal, two Newton steps, one residual step
-// (8 VALU against 13 for the IEEE-exact sequence); y finite, nonzero, normal.
+// x / y to <= 1 ulp: hardware reciprocal, one Newton step, one residual step
+// (6 VALU against 13 for the IEEE-exact sequence); y finite, nonzero, normal.
+// v_rcp_f64 is good to ~2^-25 (2.5e8 ulp measured); one Newton step brings r
+// to ~2^-50 and the residual step then rounds q as two steps would: the same
+// two_atanh on 8.4 M inputs across its domain (tools/probes/atanh_probe.hip,
+// profiles/r05/atanh_probe.json; without the Newton step 3 % differ).
 PL_DEV double div_fast(double x, double y) {
     double r = __builtin_amdgcn_rcp(y);
-    double e = fma(-y, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-y, r, 1.0);
+    const double e = fma(-y, r, 1.0);
     r = fma(r, e, r);
     const double q = x * r;
     return fma(fma(-y, q, x), r, q);

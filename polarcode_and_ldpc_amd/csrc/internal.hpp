@@ -46,11 +46,15 @@ hipError_t lane_launch(const LaneGeom& g, bool sc, const double* llr, int64_t ld
 struct TreeInfo {
     void* fn;
     void* fn_stamps;
+    void* fn_ds[2];  // PL_DIAG: dead-store record / replay instances (headline geometry only)
     int lds_bytes;
     int64_t ws_bytes;  // workspace bytes per resident wavefront
     int F, DL, fpw;
 };
 bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info);
+#if PL_DIAG
+extern int g_tree_ds_mode;  // 1 / 2: tree_launch runs the dead-store record / replay instance
+#endif
 // The tree and lane kernels' frame groups (FPW frames) past the first one per
 // wavefront come from a u32 counter in the kSchedBytes just before their
 // slices (polar_tree.hip, polar_lane.hpp); tree_launch / lane_launch zero it.
@@ -120,6 +124,7 @@ struct LdpcGeom {
     int regular;       // every check has degree maxdc and every variable degree maxdv
     int grp;           // BP reg variant: ldpc_bp_grp_kernel (degree-grouped products, padded T'/C')
     int tl;            // grp: length of the padded T'/C' arrays (doubles)
+    int npad;          // grp: pad positions listed after the variable slots (a multiple of 256, -1 filled)
 };
 struct LdpcDev {
     const int32_t* row_ptr;   // [m+1]
@@ -133,7 +138,7 @@ struct LdpcDev {
     // grp (ldpc_bp_grp_kernel): per edge slot (256 EPT of them) the T' position
     // of the edge's check | position in the check << 16 | its slot's D_s << 20;
     // per variable slot q (256 VPT of them): [q][DV] T' positions, [q][DV]
-    // checks, then [q] the variable (-1: none)
+    // checks, then [q] the variable (-1: none); then npad pad positions
     const int32_t* grp_meta;  // [256 EPT]
     const int32_t* var_tpos;  // [256 VPT (2 DV + 1)]
 };

@@ -254,10 +254,8 @@ PL_DEV void ms_prio(int i, int n) {
     else __builtin_amdgcn_s_setprio(0);
 }
 
-#ifndef PL_BP_PRIO
-// the same in ldpc_reg_kernel: +1.4 % (its SIMDs hold one wavefront of each of
-// four workgroups, which need not keep pace with each other), off
-#define PL_BP_PRIO 0
+#ifndef PL_MS_REGIDX
+#define PL_MS_REGIDX 1  // regular min-sum codes: adjacency indices cached in registers
 #endif
 
 // Register-cached variant of ldpc_decode_kernel for codes whose variable degree
@@ -265,37 +263,22 @@ PL_DEV void ms_prio(int i, int n) {
 // 256 threads, thread tid owns edges tid + j*256 (j < EPT) and variables
 // tid + j*256 (j < VPT); their edge metadata, var_edge / var_chk lists and
 // channel LLRs are loaded once into registers instead of once per iteration.
-// Same passes, barriers and arithmetic as ldpc_decode_kernel (bit-identical).
-#ifndef PL_MS_REGIDX
-#define PL_MS_REGIDX 1  // regular min-sum codes: adjacency indices cached in registers
-#endif
-#ifndef PL_BP_PROD
-#define PL_BP_PROD 0  // 1: check products over all d inputs with the own one replaced by 1.0
-#endif
-#ifndef PL_LDPC_REG_WPE
-#define PL_LDPC_REG_WPE 4  // waves per SIMD the register budget is built for
-#endif
-// FPB > 1 (diagnostic, PL_BP_FPB): FPB frames per workgroup of 256 FPB threads
-// sharing its barriers, each frame with its own LDS (g.lds_bytes apart), a
-// per-frame early-stop vote in LDS after them, frames past the batch decoding
-// the last frame again (same bytes written twice).
-template <int ALGO, int DV, int EPT, int VPT, int FPB = 1>
-__global__ void __launch_bounds__(256 * FPB) __attribute__((amdgpu_waves_per_eu(PL_LDPC_REG_WPE)))
+// Same passes and arithmetic as ldpc_decode_kernel (bit-identical).  BP on
+// codes with check degrees <= 15 runs ldpc_bp_grp_kernel below instead; this
+// one serves min-sum and the other BP codes (and PL_LDPC_KERNEL=reg).
+// Measured and not kept: products over all d inputs with the
+// own factor replaced by 1.0 (8.18 against 7.00 ms), 2 / 4 frames per
+// workgroup sharing its barriers (8.10 / 9.83), progress-based issue priority
+// (+1.4 %).
+template <int ALGO, int DV, int EPT, int VPT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
                 uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NT = 256;
-    const int fs = FPB > 1 ? (int)(threadIdx.x >> 8) : 0;
-    int64_t frame = (int64_t)blockIdx.x * FPB + fs;
-    if constexpr (FPB == 1) {
-        if (frame >= batch) return;
-    } else {
-        frame = frame < batch ? frame : batch - 1;
-    }
-    const int tid = FPB > 1 ? (int)(threadIdx.x & 255u) : (int)threadIdx.x;
-    unsigned char* const smem = smem_all + (size_t)fs * (size_t)g.lds_bytes;
-    unsigned int* const vote = reinterpret_cast<unsigned int*>(smem_all + (size_t)FPB * (size_t)g.lds_bytes);  // [2][FPB]
-    bool fdone = false;
+    const int64_t frame = blockIdx.x;
+    if (frame >= batch) return;
+    const int tid = threadIdx.x;
     const int E = g.E, n = g.n, m = g.m;
     double* T = reinterpret_cast<double*>(smem);
     double* C = T + E;
@@ -304,8 +287,7 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
     // BP: per-wavefront lists of the edges whose v2c needs a tanh (|x| <= 14.52
     // or NaN), 16-bit edge indices (E < 65536), 64*VPT*DV per wavefront: each
     // wavefront compacts and evaluates its own, so the tanh pass needs no
-    // workgroup barrier.  29 KB per frame at (504,252), so 5 frames fit a CU's
-    // LDS (capi.cpp sizes it with ldpc_reg_list_bytes)
+    // workgroup barrier (capi.cpp sizes it with ldpc_reg_list_bytes)
     uint16_t* work = reinterpret_cast<uint16_t*>(smem + (((size_t)16 * E + (size_t)8 * m + n + 15) & ~(size_t)15));
     const double* __restrict__ ch = llr + frame * ld;
     auto tin = [&](double x) -> double { return ALGO == 0 ? tanh_half_clip(x) : x; };
@@ -331,9 +313,6 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         chv[j] = ok ? ch[v] : 0.0;
     }
     for (int c = tid; c < 2 * m; c += NT) syn[c] = 0u;
-    if constexpr (FPB > 1) {
-        if (threadIdx.x < 2 * FPB) vote[threadIdx.x] = 0u;
-    }
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
         if (tid + j * NT < n) {
@@ -352,30 +331,12 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         uint32_t* scur = syn + (it & 1) * m;
         if (g.early_stop && it > 0) {
             int bad = 0;
-            if (!fdone)
-                for (int c = tid; c < m; c += NT) bad |= (int)sprev[c];
-            if constexpr (FPB == 1) {
-                if (!__syncthreads_or(bad)) { done = it; break; }
-            } else {
-                // per-frame vote: a frame whose checks all hold stops at `it`
-                // and idles (its decisions kept) until every frame has stopped
-                if (__ballot(bad) && __lane_id() == 0) atomicOr(&vote[(it & 1) * FPB + fs], 1u);
-                __syncthreads();
-                unsigned int anyb = 0;
-#pragma unroll
-                for (int f = 0; f < FPB; ++f) anyb |= vote[(it & 1) * FPB + f];
-                const bool fb = vote[(it & 1) * FPB + fs] != 0u;
-                if (threadIdx.x < FPB) vote[((it + 1) & 1) * FPB + threadIdx.x] = 0u;
-                if (!fb && !fdone) { fdone = true; done = it; }
-                if (!anyb) break;
-            }
+            for (int c = tid; c < m; c += NT) bad |= (int)sprev[c];
+            if (!__syncthreads_or(bad)) { done = it; break; }
         }
-        if (!fdone)
         for (int c = tid; c < m; c += NT) scur[c] = 0u;
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
-            if (fdone) break;
-            if constexpr (PL_BP_PRIO) ms_prio(j, EPT);
             const int e = tid + j * NT;
             if (e >= E) break;
             const int e0 = meta[j] & 0xFFFFF, d = meta[j] >> 20, i = e - e0;
@@ -389,31 +350,6 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
                 const double* hi = lo + 1;
                 const int nf = d - 1;
                 double p = 1.0;
-#if PL_DIAG && defined(PL_ABL_PROD)
-                p = lo[i == 0 ? 1 : 0];  // ablation timing build: one factor
-#else
-#if PL_BP_PROD == 1
-                // every factor at its own offset from the check's first input, the
-                // own edge's replaced by 1.0 (x * 1.0 = x exactly: the same
-                // left-to-right product), so no per-factor pointer select
-                (void)hi;
-                (void)nf;
-                int k = 0;
-                for (; k + 4 <= d; k += 4) {
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        const double f = lo[k + c];
-                        p *= (k + c == i) ? 1.0 : f;
-                    }
-                }
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    if (k + c < d) {
-                        const double f = lo[k + c];
-                        p *= (k + c == i) ? 1.0 : f;
-                    }
-                }
-#else
                 int k = 0;
                 for (; k + 4 <= nf; k += 4, lo += 4, hi += 4) {
 #pragma unroll
@@ -426,16 +362,10 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
                         if (k + 2 < nf) p *= (k + 2 < i ? lo : hi)[2];
                     }
                 }
-#endif
-#endif
                 // clip, 2*atanh, nan_to_num: after the clip 2*atanh is finite,
                 // so only a NaN product (NaN channel LLRs) maps to 0
                 const bool pn = __builtin_isnan(p);
-#if PL_DIAG && defined(PL_ABL_ATANH)
-                o = 2.0 * __builtin_fmax(__builtin_fmin(p, 0.999999), -0.999999);  // ablation: no atanh
-#else
                 o = two_atanh(__builtin_fmax(__builtin_fmin(p, 0.999999), -0.999999));
-#endif
                 o = pn ? 0.0 : o;
             } else {
                 o = ms_check(T + e0, i, d, g.norm);
@@ -447,8 +377,6 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         int wn = 0;                                                 // its length (wavefront-uniform)
 #pragma unroll
         for (int j = 0; j < VPT; ++j) {
-            if (fdone) break;
-            if constexpr (PL_BP_PRIO) ms_prio(j, VPT);
             const int v = tid + j * NT;
             const bool vok = v < n;  // lanes past n run along (ve = 0) with every store masked
             if (!__ballot(vok)) break;
@@ -487,13 +415,9 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
             // runs a wavefront's operations in order: no barrier
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            for (int w = lane; w < wn; w += 64) {  // wn = 0 for a stopped frame
+            for (int w = lane; w < wn; w += 64) {
                 const int e = wl[w];
-#if PL_DIAG && defined(PL_ABL_TANH)
-                T[e] = 0.5 * T[e];  // ablation timing build: no tanh
-#else
                 T[e] = tanh_half_clip(T[e]);
-#endif
             }
         }
         __syncthreads();  // T and the syndrome parities for the next iteration's vote / check pass
@@ -620,8 +544,14 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
     }
     for (int c = tid; c < mp; c += NT) syn[c] = 0u;  // H * 0
     uint32_t decs = 0;  // bit j: the decision of variable tid + 256 j (initially 0)
-    for (int q = tid; q < tl; q += NT) T[q] = 1.0;  // the pads
-    __syncthreads();
+    {
+        // the pads (positions no edge writes: no barrier before the edges' writes)
+        const int32_t* __restrict__ pads = dv.var_tpos + (2 * DV + 1) * NT * VPT;
+        for (int q = tid; q < g.npad; q += NT) {
+            const int x = pads[q];
+            if (x >= 0) T[x] = 1.0;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
         if (vid[j] >= 0) {
@@ -637,7 +567,6 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
     PL_GSTAMP(0)
     int done = g.max_iter;
     for (int it = 0; it < g.max_iter; ++it) {
-#ifndef PL_ABL_VOTE
         if (g.early_stop && it > 0) {
             // every wavefront reads all m parities itself (the previous closing
             // barrier made them complete) and reaches the same verdict: no
@@ -653,7 +582,6 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
             }
             if (!__ballot(bad != 0u)) { done = it; break; }
         }
-#endif
         PL_GSTAMP(1)
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
@@ -684,7 +612,7 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
             const bool pn = __builtin_isnan(p);
             double o = two_atanh(__builtin_fmax(__builtin_fmin(p, 0.999999), -0.999999));
             o = pn ? 0.0 : o;
-            if (i != 15) C[base + i] = o;  // 15: no edge in this lane of the slot
+            C[base + i] = o;  // lanes without an edge: the sink
         }
         PL_GSTAMP(2)
         __syncthreads();
@@ -717,9 +645,7 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)nb, 0u));
                 if (need) wl[wn + pre] = (uint16_t)ve[j][k];
                 wn += (int)__popcll(nb);
-#ifndef PL_ABL_SYN
                 if (flip) atomicXor(&syn[vc[j][k]], 1u);
-#endif
             }
         }
         PL_GSTAMP(4)
@@ -748,13 +674,6 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
 
 // (DV, EPT, VPT) instances of ldpc_reg_kernel: E <= 256*EPT, n <= 256*VPT
 struct RegVariant { int dv, ept, vpt; void* k[3]; };  // BP, MS, BP degree-grouped
-#if PL_DIAG
-static void* reg_fpb_kernel(int fpb, int algo) {  // diagnostic FPB instances of the (3, 6, 2) variant
-    if (fpb == 2) return algo == 0 ? (void*)ldpc_reg_kernel<0, 3, 6, 2, 2> : (void*)ldpc_reg_kernel<1, 3, 6, 2, 2>;
-    if (fpb == 4) return algo == 0 ? (void*)ldpc_reg_kernel<0, 3, 6, 2, 4> : (void*)ldpc_reg_kernel<1, 3, 6, 2, 4>;
-    return nullptr;
-}
-#endif
 template <int DV, int EPT, int VPT>
 static RegVariant reg_variant() {
     return {DV, EPT, VPT,
@@ -1301,13 +1220,6 @@ static void* pick_kernel(const LdpcGeom& g) {
     return g.algo == 0 ? pick<0>(g.use_global) : pick<1>(g.use_global);
 }
 
-#if PL_DIAG
-static int bp_fpb(const LdpcGeom& g) {  // PL_BP_FPB=2|4: the reg (3, 6, 2) variant with FPB frames per workgroup
-    static const int v = [] { const char* e = std::getenv("PL_BP_FPB"); return e ? std::atoi(e) : 1; }();
-    return (v == 2 || v == 4) && g.reg_variant == 1 ? v : 1;
-}
-static size_t fpb_lds(const LdpcGeom& g, int f) { return (size_t)f * (((size_t)g.lds_bytes + 15) & ~(size_t)15) + 64; }
-#endif
 
 #if PL_DIAG
 // the degree-grouped BP kernel of a grp plan with per-phase stamps (4 x 8 u64)
@@ -1325,11 +1237,6 @@ hipError_t ldpc_launch_stamped(const LdpcGeom& g, const LdpcDev& d, const double
 #endif
 
 hipError_t ldpc_prepare(const LdpcGeom& g) {
-#if PL_DIAG
-    if (int f = bp_fpb(g); f > 1)
-        return hipFuncSetAttribute(reg_fpb_kernel(f, g.algo), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)fpb_lds(g, f));
-#endif
     void* k = pick_kernel(g);
     return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds_bytes);
 }
@@ -1341,14 +1248,6 @@ hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, i
     LdpcDev dd = d;
     void* args[] = {&gg, &dd, (void*)&llr, (void*)&ld, (void*)&bits, (void*)&iters, (void*)&batch,
                     (void*)&work};
-#if PL_DIAG
-    if (int f = bp_fpb(g); f > 1) {
-        gg.lds_bytes = (int)(((size_t)g.lds_bytes + 15) & ~(size_t)15);  // per-frame LDS stride
-        void* args7[] = {&gg, &dd, (void*)&llr, (void*)&ld, (void*)&bits, (void*)&iters, (void*)&batch};
-        return hipLaunchKernel(reg_fpb_kernel(f, g.algo), dim3((unsigned)((batch + f - 1) / f)), dim3(256 * f), args7,
-                               fpb_lds(g, f), s);
-    }
-#endif
     return hipLaunchKernel(k, dim3((unsigned)batch), dim3(g.threads), args, g.lds_bytes, s);
 }
 

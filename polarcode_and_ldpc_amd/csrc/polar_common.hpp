@@ -64,11 +64,7 @@ PL_DEV void path_metrics_fast(double pm, double lam, bool active, double& m0, do
     const bool skip = !active || (!finite_pm && !__builtin_isnan(x)) ||
                       (finite_pm && pm != 0.0 && x > (double)(57 - e) * 0.6931471805599453);
     double t = 0.0;
-#if PL_DIAG && defined(PL_ABL_METRIC)
-    (void)skip;  // ablation timing build: no transcendental (decisions change)
-#else
     if (!skip) t = FUSED ? log1p_exp_neg(x) : log1p_pos(exp_neg(x));  // lean exp / log1p (fp64_math.hpp)
-#endif
     m0 = pm + ((lam >= 0.0) ? -t : lam - t);
     if (WANT1) m1 = pm + ((lam >= 0.0) ? -lam - t : -t);
 }

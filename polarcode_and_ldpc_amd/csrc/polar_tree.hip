@@ -53,23 +53,11 @@ namespace {
 #ifndef RANK_STRICT_LCAP
 #define RANK_STRICT_LCAP 8  // list capacities ranked with strict comparisons
 #endif
-#ifndef PL_TREE_DYN
-#define PL_TREE_DYN 1  // frame groups past the first claimed from a counter (the kernel's group loop)
-#endif
 #ifndef PL_TREE_PRIO
 // issue priority (s_setprio) against the SIMD's age-ordered arbitration: 1 =
 // a group claimed in the last quarters of its round runs at priority 1..3;
 // 2 = also the first group by dispatch quarter (kernel: group loop)
 #define PL_TREE_PRIO 2
-#endif
-#ifndef PL_RATE0
-#define PL_RATE0 2  // rate-0 nodes of 2..8 leaves decoded at their first leaf; >= 2: metric chains per group
-#endif
-#ifndef PL_ABL_RANK
-#define PL_ABL_RANK 0  // diagnostic ablation (PL_DIAG only): fake ranks
-#endif
-#ifndef PL_RANK_BITONIC
-#define PL_RANK_BITONIC 1  // LCAP = 32: survivors by a lane-exchange bitonic sort (collisions fall back)
 #endif
 #ifndef PL_ORDERED_PRUNE
 #define PL_ORDERED_PRUNE 16  // list capacities >= this skip ranking when the full list stays ordered (ordered_prune)
@@ -90,9 +78,6 @@ namespace {
 #endif
 #ifndef PL_DEDUP_NMAX
 #define PL_DEDUP_NMAX 10  // largest n whose fused top de-duplicates its staged reads
-#endif
-#ifndef PL_RANK_F32
-#define PL_RANK_F32 1  // strict ranks from fp32 roundings of the metrics (collisions fall back)
 #endif
 
 // Lane exchanges inside the 8-lane group of a frame (LCAP = 8) without LDS:
@@ -221,9 +206,10 @@ PL_DEV bool ordered_prune(double m0, double m1, int slot, int lane) {
 
 constexpr int RB = 5;  // bits per slot field of a pointer row (list capacity <= 32)
 
-template <int NL, int LCAP_, int F_, int DL_>
+template <int NL, int LCAP_, int F_, int DL_, int DS_ = 0>
 struct TG {
     static constexpr int n = NL, N = 1 << NL, LCAP = LCAP_, FPW = 64 / LCAP_, F = F_, DL = DL_;
+    static constexpr int DS = DS_;  // dead-store record / replay instance (diagnostic, kernel comment)
     static constexpr int CW = N / 32;
     static constexpr int NB = n - 6;          // multi-word beta depths 1..NB (workspace)
     static constexpr bool STAGE = LCAP > 1;   // stage channel rows shared by a frame's lanes
@@ -324,6 +310,7 @@ template <class G>
 struct Fold {
     double pend[G::n + 1];  // pending even element per depth
     double lam;             // the leaf LLR (depth n)
+    uint32_t skip;          // G::DS == 2 only: bit d = do not store depth d (dead-store bound)
 };
 
 // Element idx of depth D has been computed: if even, hold it; if odd, store the
@@ -336,7 +323,7 @@ PL_DEV void fold(Fold<G>& st, double v, int idx, unsigned char* smem, unsigned c
     } else {
         if (idx & 1) {
             double2* dst = reinterpret_cast<double2*>((D >= G::DL ? smem : ws) + G::llr_off(D));
-            dst[(idx >> 1) * 64 + plane] = make_double2(st.pend[D], v);
+            if (G::DS != 2 || !((st.skip >> D) & 1u)) dst[(idx >> 1) * 64 + plane] = make_double2(st.pend[D], v);
             fold<G, D + 1>(st, f_ms(st.pend[D], v), idx >> 1, smem, ws, plane);
         } else {
             st.pend[D] = v;
@@ -348,10 +335,11 @@ PL_DEV void fold(Fold<G>& st, double v, int idx, unsigned char* smem, unsigned c
 // sibling's partial sums, then the f-chain down to the leaf.
 template <class G, int P>
 PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int plane, int ps, int bs, uint32_t bb,
-                        uint32_t bw5) {
+                        uint32_t bw5, uint32_t skip) {
     constexpr int n = G::n, Q = P + 1, SQ = 1 << (n - Q);
     Fold<G> st;
     st.lam = 0.0;
+    if constexpr (G::DS == 2) st.skip = skip;
     const double2* src = reinterpret_cast<const double2*>((P >= G::DL ? smem : ws) + G::llr_off(P)) + ps;
     uint32_t w = 0;
     if constexpr (Q > G::NB) w = beta_get<n>(Q, bb, bw5);
@@ -381,10 +369,12 @@ PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int plane, int p
 // depth-d ancestor of leaf i is a right child), then the f-chain to the leaf.
 template <class G, int D0>
 PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int fw, int plane, const double* ch,
-                         const double2* raw, const bool* right, const uint32_t* const* bsrc, uint32_t* bw) {
+                         const double2* raw, const bool* right, const uint32_t* const* bsrc, uint32_t* bw,
+                         uint32_t skip) {
     constexpr int n = G::n, F = G::F, SF = 1 << (n - F), W = 1 << (F - D0);
     Fold<G> st;
     st.lam = 0.0;
+    if constexpr (G::DS == 2) st.skip = skip;
     if constexpr (G::dedup(D0)) {
         // De-duplicated staged reads: the staged depth is [S/2][FPW] pairs, so
         // a 1 KB chunk (LCAP pairs of every frame of the wave) is contiguous.
@@ -508,7 +498,8 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
 
 template <class G>
 PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, int fw, int plane, int i,
-                            const double* ch, const double2* raw, uint64_t brow, uint32_t bb, uint32_t bw5) {
+                            const double* ch, const double2* raw, uint64_t brow, uint32_t bb, uint32_t bw5,
+                            uint32_t skip = 0) {
     constexpr int n = G::n, F = G::F;
     bool right[F + 1];
     const uint32_t* bsrc[F + 1];
@@ -521,15 +512,15 @@ PL_DEV double descend_fused(unsigned char* smem, unsigned char* ws, int lane, in
         bw[d] = (d > G::NB) ? beta_get<n>(d, bb, bw5) : 0u;
     }
     if constexpr (G::NS >= 3) {
-        if (!right[1] && !right[2] && !right[3]) return fused_loop<G, 3>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw);
+        if (!right[1] && !right[2] && !right[3]) return fused_loop<G, 3>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw, skip);
     }
     if constexpr (G::NS >= 2) {
-        if (!right[1] && !right[2]) return fused_loop<G, 2>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw);
+        if (!right[1] && !right[2]) return fused_loop<G, 2>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw, skip);
     }
     if constexpr (G::NS >= 1) {
-        if (!right[1]) return fused_loop<G, 1>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw);
+        if (!right[1]) return fused_loop<G, 1>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw, skip);
     }
-    return fused_loop<G, 0>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw);
+    return fused_loop<G, 0>(smem, ws, lane, fw, plane, ch, raw, right, bsrc, bw, skip);
 }
 
 // Size 2^k (k <= 3) of the rate-0 node (all leaves frozen) whose first leaf is
@@ -580,11 +571,10 @@ PL_DEV void rate0_rest(const unsigned char* smem, const unsigned char* ws, int p
             a[2 * j + 1] = pr.y;
         }
         rate0_leaves<S>(a, ll);
-#if PL_RATE0 >= 2
-        // increments of PL_RATE0 leaves evaluated together (independent chains),
+        // increments of two leaves evaluated together (independent chains),
         // always computed: where path_metrics_fast skips t it is below a quarter
         // ulp of every addend and the sums are the same
-        constexpr int IL = PL_RATE0;
+        constexpr int IL = 2;
 #pragma unroll
         for (int j0 = 1; j0 < S; j0 += IL) {
             double inc[IL];
@@ -592,11 +582,7 @@ PL_DEV void rate0_rest(const unsigned char* smem, const unsigned char* ws, int p
             for (int u = 0; u < IL; ++u) {
                 if (j0 + u < S) {
                     const double lam = ll[j0 + u];
-#if PL_DIAG && defined(PL_ABL_METRIC)
-                    const double t = 0.0 * lam;
-#else
                     const double t = G::n <= PL_METRIC_FUSED_NMAX ? log1p_exp_neg(fabs(lam)) : log1p_pos(exp_neg(fabs(lam)));
-#endif
                     inc[u] = (lam >= 0.0) ? -t : lam - t;
                 }
             }
@@ -604,31 +590,28 @@ PL_DEV void rate0_rest(const unsigned char* smem, const unsigned char* ws, int p
             for (int u = 0; u < IL; ++u)
                 if (j0 + u < S && active) pm = pm + inc[u];
         }
-#else
-#pragma unroll
-        for (int j = 1; j < S; ++j) {
-            double m0, m1;
-            path_metrics_fast<false, (G::n <= PL_METRIC_FUSED_NMAX)>(pm, ll[j], active, m0, m1);
-            if (active) pm = m0;
-        }
-#endif
     }
 }
 
 template <class G, int P>
 PL_DEV double descend_from(int p, unsigned char* smem, unsigned char* ws, int plane, int ps, int bs, uint32_t bb,
-                           uint32_t bw5) {
+                           uint32_t bw5, uint32_t skip = 0) {
     if constexpr (P >= G::n) {
         return 0.0;
     } else {
-        if (p == P) return descend_g<G, P>(smem, ws, plane, ps, bs, bb, bw5);
-        return descend_from<G, P + 1>(p, smem, ws, plane, ps, bs, bb, bw5);
+        if (p == P) return descend_g<G, P>(smem, ws, plane, ps, bs, bb, bw5, skip);
+        return descend_from<G, P + 1>(p, smem, ws, plane, ps, bs, bb, bw5, skip);
     }
 }
 
 }  // namespace
 
-template <int NL, int LCAP, bool SC, int F, int DL, bool STAMPS, int WPE>
+// DS (diagnostic build, the dead-store bound of DESIGN.md §4.1): 1 records in
+// `stamps` (u32 words, [group][read, stored][node of depths F..DL-1][64 planes]
+// bits) every workspace pool array a right child's g reads and every one
+// stored; 2 replays the same frames with every store of an unread array
+// skipped (same bits by construction).
+template <int NL, int LCAP, bool SC, int F, int DL, bool STAMPS, int WPE, int DS = 0>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restrict__ out,
                   const uint32_t* __restrict__ frozen_dec, const int32_t* __restrict__ info_pos, int64_t batch,
@@ -639,7 +622,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
     // words it reads).  One argument for both: a separate mask pointer kept live
     // across the leaf loop cost the list instances 8-24 spilled bytes per lane.
     const uint32_t* __restrict__ r0k = SC ? aux : nullptr;
-    using G = TG<NL, LCAP, F, DL>;
+    using G = TG<NL, LCAP, F, DL, DS>;
     constexpr int n = G::n, N = G::N, FPW = G::FPW;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
@@ -651,13 +634,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
     // every pruning (same rows, partial sums and bit; metric -inf), uses slot
     // 0's plane, and so loads the lines slot 0 loads and stores the values
     // slot 0 stores to the same addresses -- no memory traffic of its own.
-#if PL_DIAG && defined(PL_ABL_WSMASK)
-    // ablation timing build: every wave shares one of PL_ABL_WSMASK+1 slices, so
-    // the pools stay in L2 (wrong bits, same instruction stream)
-    unsigned char* const ws = workspace + (size_t)(blockIdx.x & PL_ABL_WSMASK) * G::WS;
-#else
     unsigned char* const ws = workspace + (size_t)blockIdx.x * G::WS;
-#endif
     uint64_t own = 0;
 #pragma unroll
     for (int d = 0; d < 12; ++d) own |= (uint64_t)slot << (RB * d);
@@ -676,15 +653,13 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         tprev = tn;                                                 \
     }
 
-    // Frame groups (FPW frames each): group blockIdx.x first; then, with
-    // PL_TREE_DYN, the next unclaimed group from one counter (kSchedBytes
-    // before the slices, zeroed by tree_launch), so that wavefronts slowed by
-    // harder frames, a busier SIMD or a busier XCD take fewer groups instead of
-    // stretching the launch's tail; else groups b, b + grid, b + 2 grid, ...
+    // Frame groups (FPW frames each): group blockIdx.x first; then the next
+    // unclaimed group from one counter (kSchedBytes before the slices, zeroed by
+    // tree_launch), so that wavefronts slowed by harder frames, a busier SIMD or
+    // a busier XCD take fewer groups instead of stretching the launch's tail
+    // (the static b, b + grid, b + 2 grid, ... measured 8.5 % slower at L = 32)
     const int64_t ngrp = (batch + FPW - 1) / FPW;
-#if PL_TREE_DYN
     unsigned int* const sched = reinterpret_cast<unsigned int*>(workspace - kSchedBytes);
-#endif
     // (not at n = 12, whose launches are bound by memory bandwidth: +3 % at
     // 131 072 frames, profiles/r04_a/ab_prio_4096.log)
     constexpr int PRIO = G::n <= 11 ? PL_TREE_PRIO : 0;
@@ -711,13 +686,17 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
             constexpr int CV = 2 << G::NS;    // channel values per lane per step
             constexpr int CPI = 64 / FPW;     // chunks per frame per step
             // NaN path metrics need a NaN LLR at a leaf, i.e. a NaN input or an
-            // inf - inf in a g; with every |input| < 2^1000 (and none NaN) each of
-            // the <= 12 levels at most doubles a magnitude, so every LLR is finite
-            // and every metric a sum of finite non-positive terms (-inf at worst,
-            // never NaN).  Frames with a NaN or |input| >= 2^1000 are flagged in
-            // this pass's mask word (aux) and decoded again by polar_nan.hip in the
-            // reference's exact candidate order (list.sort, decoder.py:306-307).
-            bool ext = false;
+            // inf - inf in a g.  The two operands of a g descend from disjoint
+            // halves of its node's inputs, and an LLR whose inputs are all below
+            // 2^1000 in magnitude is finite (<= 12 levels at most double it), so
+            // with no NaN input and at most ONE input of magnitude >= 2^1000 (or
+            // inf) no g meets two infinities: every LLR is finite or +-inf and
+            // every metric a sum of non-positive terms (-inf at worst, never NaN).
+            // Frames with a NaN input or two such inputs are flagged in this
+            // pass's mask word (aux) and decoded again by polar_nan.hip in the
+            // reference's exact candidate order (list.sort, decoder.py:306-307);
+            // a frame with one erasure-style +-inf stays on this kernel.
+            int ext = 0;  // this lane's inputs of magnitude >= 2^1000 or inf, + 2 per NaN
 #pragma unroll 1
             for (int cb = 0; cb < N / CV; cb += CPI) {
                 const int cc = cb + lane / FPW;
@@ -725,7 +704,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
 #pragma unroll
                 for (int k = 0; k < CV; ++k) v[k] = row[CV * cc + k];
 #pragma unroll
-                for (int k = 0; k < CV; ++k) ext |= !(fabs(v[k]) < 0x1p1000);
+                for (int k = 0; k < CV; ++k) ext += !(fabs(v[k]) < 0x1p1000) ? (__builtin_isnan(v[k]) ? 2 : 1) : 0;
                 // depth d of the chunk: CV >> d values = CV >> (d+1) pairs
 #pragma unroll
                 for (int d = 0; d <= G::NS; ++d) {
@@ -741,15 +720,21 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     }
                 }
             }
-            const uint64_t bal = __ballot(ext);  // lane l stages frame l % FPW
-            if (!SC && bal) {
+            // lane l stages frame l % FPW: a frame is flagged when a lane saw a NaN
+            // or two extreme inputs, or two of its lanes saw one each
+            const uint64_t b1 = __ballot(ext >= 1), b2 = __ballot(ext >= 2);
+            if (!SC && b1) {
+                uint64_t lanes = 0;
+#pragma unroll
+                for (int sft = 0; sft < 64; sft += FPW) lanes |= 1ull << sft;
                 uint64_t fm = 0;
 #pragma unroll
-                for (int sft = 0; sft < 64; sft += FPW) fm |= (bal >> sft) & ((1ull << FPW) - 1ull);
+                for (int f = 0; f < FPW; ++f)
+                    if ((b2 & (lanes << f)) || __popcll(b1 & (lanes << f)) >= 2) fm |= 1ull << f;
                 // word [grp % grid][grp / grid], where the static schedule's pass
                 // grp / grid of wavefront grp % grid keeps it (polar_nan.hip)
                 const uint32_t ps = (uint32_t)grp / gridDim.x, wv = (uint32_t)grp % gridDim.x;
-                if (lane == 0 && ps < (uint32_t)kNanMaskPasses)
+                if (fm && lane == 0 && ps < (uint32_t)kNanMaskPasses)
                     atomicOr(reinterpret_cast<unsigned long long*>(const_cast<uint32_t*>(aux)) +
                                  (size_t)wv * kNanMaskPasses + ps,
                              (unsigned long long)fm);
@@ -778,18 +763,48 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
             const int skipK = SC ? nextK : 0;
             const bool skip_descend = SC && skipK > 0 && i > 0 && skipK >= __builtin_ctz(i);
             double lam = 0.0;
+            // DS: the pool arrays of node i >> (n - d), depths F..DL-1, as bits of
+            // this group's words: [read][stored], DSW words each
+            constexpr int DSW = ((1 << DL) - (1 << F)) * 2;
+            uint32_t* const dsm = DS ? reinterpret_cast<uint32_t*>(stamps) + grp * 2 * DSW : nullptr;
+            uint32_t dskip = 0;
+            if constexpr (DS == 1) {
+                if (!skip_descend) {
+#pragma unroll
+                    for (int d = F; d < DL; ++d)
+                        if (d >= dstart)
+                            atomicOr(dsm + DSW + ((1 << d) - (1 << F) + (i >> (n - d))) * 2 + (plane >> 5),
+                                     1u << (plane & 31));
+                }
+            }
+            if constexpr (DS == 2) {
+                // (depth, node) is wave-uniform: one scalar 8-byte load per depth,
+                // the lane's plane bit extracted from it (no per-lane gather)
+                const uint64_t* __restrict__ dsm64 = reinterpret_cast<const uint64_t*>(stamps) + grp * DSW;
+#pragma unroll
+                for (int d = F; d < DL; ++d) {
+                    if (d >= dstart) {
+                        const uint64_t mk = dsm64[(1 << d) - (1 << F) + (i >> (n - d))];
+                        if (!((mk >> plane) & 1u)) dskip |= 1u << d;
+                    }
+                }
+            }
             if (!skip_descend) {
                 if (dstart <= DL) ws_sync();  // workspace written by other lanes
                 STAMP(7);
                 if (dstart <= F) {
-                    lam = descend_fused<G>(smem, ws, lane, fw, plane, i, ch, raw, brow, bb, bw5);
+                    lam = descend_fused<G>(smem, ws, lane, fw, plane, i, ch, raw, brow, bb, bw5, dskip);
                     lrow = set_range(lrow, (!G::SHADOW || slot < nact) ? own : 0ull, F, n);
                     STAMP(0);
                 } else {
                     const int p = dstart - 1;
                     const int ps = G::pl(field(lrow, p), fw);
                     const int bs = G::pl(field(brow, dstart <= G::NB ? dstart : 0), fw);
-                    lam = descend_from<G, F>(p, smem, ws, plane, ps, bs, bb, bw5);
+                    if constexpr (DS == 1) {
+                        if (p >= F && p < DL)
+                            atomicOr(dsm + ((1 << p) - (1 << F) + (i >> (n - p))) * 2 + (ps >> 5), 1u << (ps & 31));
+                    }
+                    lam = descend_from<G, F>(p, smem, ws, plane, ps, bs, bb, bw5, dskip);
                     lrow = set_range(lrow, (!G::SHADOW || slot < nact) ? own : 0ull, dstart, n);
                     if (p < DL) { STAMP(1); } else { STAMP(2); }
                 }
@@ -824,14 +839,14 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     pm = bit ? m1 : m0;
                 } else {
                 constexpr bool STRICT = LCAP >= RANK_STRICT_LCAP || NL >= 11;
-                constexpr bool F32 = STRICT && PL_RANK_F32;
+                constexpr bool F32 = STRICT;
                 // DPP: the fp32 ranks from lane exchanges inside the frame's 8
                 // lanes instead of an LDS round trip (N=1024 6.42 -> 6.38 ms,
                 // N=4096 11.69 -> 11.51 ms).  Finding each survivor the same way
                 // (a search over the 8 lanes' ranks instead of the LDS survivor
                 // table) measured slower: 6.52 ms.
                 constexpr bool DPP = F32 && LCAP == 8;
-                constexpr bool BITONIC = F32 && LCAP == 32 && PL_RANK_BITONIC && !(PL_DIAG && PL_ABL_RANK);
+                constexpr bool BITONIC = F32 && LCAP == 32;
                 if constexpr (F32 && !DPP && !BITONIC) reinterpret_cast<float2*>(met)[slot] = make_float2((float)m0, (float)m1);
                 else met[slot] = make_double2(m0, m1);
                 rowx[2 * slot] = lrow;
@@ -912,10 +927,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                     // the survivors cannot hide one below them.
                     r0 = 0;
                     r1 = 0;
-                    if constexpr (PL_DIAG && PL_ABL_RANK) {
-                        r0 = 2 * slot;  // ablation timing build: no ranking (decisions change)
-                        r1 = 2 * slot + 1;
-                    } else if constexpr (DPP) {
+                    if constexpr (DPP) {
                         const float f0 = (float)m0, f1 = (float)m1;
                         r0 = f1 > f0;  // own pair (f0 > f0 never counts)
                         r1 = f0 > f1;
@@ -1016,7 +1028,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
             if constexpr (SC) {
                 if (skipK > 0) i += (1 << skipK) - 1;  // the walk below runs for the node's last leaf
                 nextK = (r0k && i + 1 < N) ? (int)((r0k[(i + 1) >> 3] >> (4 * ((i + 1) & 7))) & 15u) : 0;
-            } else if constexpr (PL_RATE0 != 0) {
+            } else {
                 if (frozen) {
                     const int k = rate0_k(frozen_dec, i);
                     if (k > 0) {
@@ -1185,7 +1197,6 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         lds_sync();
         ws_sync();  // staging of the next frames overwrites workspace read above
         STAMP(6);
-#if PL_TREE_DYN
         // a counter read past the end (it only grows: a stale value is never
         // too large) ends the loop without a claim, so the wavefronts finishing
         // together at the end do not queue on one atomic
@@ -1202,11 +1213,8 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
         // its round runs the next group at a higher issue priority
         if (PRIO >= 1 && nx != 0xFFFFFFFFu) set_prio_quarter(nx % gridDim.x, gridDim.x);
 #endif
-#else
-        grp += gridDim.x;
-#endif
     }
-    if constexpr (STAMPS) {
+    if constexpr (STAMPS && !DS) {
         if (lane == 0)
             for (int k = 0; k < 8; ++k) atomicAdd(stamps + k, acc[k]);
     }
@@ -1223,6 +1231,7 @@ struct TreeEntry {
     void* fn;         // compiled for 4 waves/SIMD (<= 128 VGPRs; measured fastest)
     void* fn_stamps;  // PL_DIAG only: per-phase s_memtime stamps
     void* fn_wpe1;    // PL_DIAG only: compiler's own register budget (3 waves/SIMD), PL_TREE_WPE=1
+    void* fn_ds[2];   // PL_DIAG only (the headline instance): dead-store record / replay
     int lds;
     int64_t ws;
 };
@@ -1232,12 +1241,18 @@ TreeEntry make_entry() {
     using G = TG<NL, LCAP, F, DL>;
     void* st = nullptr;
     void* w1 = nullptr;
+    void* ds1 = nullptr;
+    void* ds2 = nullptr;
 #if PL_DIAG
     st = (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, true, WPE>;
-    if constexpr (VARIANTS) w1 = (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 1>;
+    if constexpr (VARIANTS) {
+        w1 = (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, 1>;
+        ds1 = (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, WPE, 1>;
+        ds2 = (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, WPE, 2>;
+    }
 #endif
     return TreeEntry{NL, LCAP, SC, F, DL, (void*)polar_tree_kernel<NL, LCAP, SC, F, DL, false, WPE>, st, w1,
-                     G::LDS, G::WS};
+                     {ds1, ds2}, G::LDS, G::WS};
 }
 
 // (n, list capacity) pairs built with the tree kernel: the BASELINE.json
@@ -1293,6 +1308,10 @@ const TreeEntry* tree_table(int* count) {
 
 }  // namespace
 
+#if PL_DIAG
+int g_tree_ds_mode = 0;
+#endif
+
 bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info) {
     int cnt = 0;
     const TreeEntry* t = tree_table(&cnt);
@@ -1308,6 +1327,8 @@ bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info) {
             const int wpe = w ? std::atoi(w) : 4;
             info->fn = (wpe == 1 && t[k].fn_wpe1) ? t[k].fn_wpe1 : t[k].fn;
             info->fn_stamps = t[k].fn_stamps;
+            info->fn_ds[0] = t[k].fn_ds[0];
+            info->fn_ds[1] = t[k].fn_ds[1];
             info->lds_bytes = t[k].lds;
             info->ws_bytes = t[k].ws;
             info->F = t[k].F;
@@ -1337,12 +1358,20 @@ hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t
                        unsigned long long* stamps, const uint32_t* crc_g, const void* aux, hipStream_t s) {
     void* args[] = {(void*)&llr, (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos, (void*)&batch,
                     (void*)&K,   (void*)&Lsz, (void*)&ws, (void*)&stamps,     (void*)&crc_g,    (void*)&aux};
-    if (stamps && !t.fn_stamps) return hipErrorInvalidValue;
-#if PL_TREE_DYN
+    void* fn = stamps ? t.fn_stamps : t.fn;
+#if PL_DIAG
+    if (g_tree_ds_mode) {  // pl_debug_polar_deadstore: `stamps` is the record / replay bitmask
+        fn = t.fn_ds[g_tree_ds_mode - 1];
+        if (!fn || !stamps) return hipErrorInvalidValue;
+        if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, t.lds_bytes);
+            e != hipSuccess)
+            return e;
+    }
+#endif
+    if (!fn) return hipErrorInvalidValue;
     // the frame-group counter (kernel: group loop)
     if (hipError_t e = hipMemsetAsync(ws - kSchedBytes, 0, 4, s); e != hipSuccess) return e;
-#endif
-    return hipLaunchKernel(stamps ? t.fn_stamps : t.fn, dim3((unsigned)grid), dim3(64), args, t.lds_bytes, s);
+    return hipLaunchKernel(fn, dim3((unsigned)grid), dim3(64), args, t.lds_bytes, s);
 }
 
 }  // namespace pl

@@ -409,7 +409,7 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
             g.threads = 256;
             // + the per-wavefront BP tanh lists (ldpc_reg_kernel)
             const size_t base = ((size_t)2 * E * 8 + lds_small + 15) & ~(size_t)15;
-            g.lds_bytes = (int)((base + pl::ldpc_reg_list_bytes(g.reg_variant) + 15) & ~(size_t)15);
+            g.lds_bytes = (int)((base + pl::ldpc_reg_list_bytes(g.reg_variant) + 15) & ~(size_t)15) + 128;  // + vote words
         }
     }
     // BP on a reg variant: degree-grouped check products (ldpc_bp_grp_kernel).
@@ -489,7 +489,7 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     // min-sum codes whose T/C arrays exceed LDS: compressed check state in LDS
     g.compact = 0;
     if (g.use_global && algo == 1 && maxdc <= 15 && !(lk && std::string(lk) == "generic")) {
-        const size_t lds_c = (((size_t)8 * n + 15) & ~(size_t)15) + (size_t)20 * m;
+        const size_t lds_c = (((((size_t)8 * n + 15) & ~(size_t)15) + (size_t)20 * m + 15) & ~(size_t)15) + 128;  // + vote words
         if (lds_c <= 160 * 1024) {
             g.compact = 1;
             g.use_global = 0;

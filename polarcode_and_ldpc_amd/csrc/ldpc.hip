@@ -38,6 +38,26 @@ PL_DEV double clip999(double x) {
 }
 
 
+// OR of `pred` over the workgroup behind one barrier (__syncthreads_or costs
+// three: a reduction, then two barriers around an LDS word): each wavefront's
+// ballot goes to its own LDS word, words[parity][wave] (double-buffered by the
+// caller's iteration parity, so a word is rewritten only after every wavefront
+// has passed the barriers of the iteration that read it), then every thread
+// reads them all.  words: 2 * 16 u32 of LDS.
+PL_DEV bool wg_any(bool pred, uint32_t* words, int parity) {
+    const bool any_w = __ballot(pred) != 0;
+    if (__lane_id() == 0) words[parity * 16 + (threadIdx.x >> 6)] = any_w ? 1u : 0u;
+    __syncthreads();
+    const uint4* w4 = reinterpret_cast<const uint4*>(words + parity * 16);
+    uint32_t any = 0;
+    const int nw4 = (blockDim.x + 255) >> 8;  // wavefronts / 4
+    for (int k = 0; k < nw4; ++k) {
+        const uint4 v = w4[k];
+        any |= v.x | v.y | v.z | v.w;
+    }
+    return any != 0u;
+}
+
 // 2*atanh(p), |p| <= 0.999999 (after the reference's clip), NaN -> NaN.
 // 2 atanh(a) = log(y), y = (1+a)/(1-a) = 2^k m, m in [sqrt(2)/2, sqrt(2)) with k
 // from an fp32 estimate of y; log(m) = 2s + s R(s^2) (the fdlibm log kernel),
@@ -289,6 +309,7 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
     // wavefront compacts and evaluates its own, so the tanh pass needs no
     // workgroup barrier (capi.cpp sizes it with ldpc_reg_list_bytes)
     uint16_t* work = reinterpret_cast<uint16_t*>(smem + (((size_t)16 * E + (size_t)8 * m + n + 15) & ~(size_t)15));
+    uint32_t* vote = reinterpret_cast<uint32_t*>(smem + g.lds_bytes - 128);  // [2][16] (wg_any)
     const double* __restrict__ ch = llr + frame * ld;
     auto tin = [&](double x) -> double { return ALGO == 0 ? tanh_half_clip(x) : x; };
     const int lane = __lane_id();
@@ -332,7 +353,7 @@ ldpc_reg_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t 
         if (g.early_stop && it > 0) {
             int bad = 0;
             for (int c = tid; c < m; c += NT) bad |= (int)sprev[c];
-            if (!__syncthreads_or(bad)) { done = it; break; }
+            if (!wg_any(bad != 0, vote, it & 1)) { done = it; break; }
         }
         for (int c = tid; c < m; c += NT) scur[c] = 0u;
 #pragma unroll
@@ -857,6 +878,7 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
     double* tot = reinterpret_cast<double*>(smem);
     double2* smin = reinterpret_cast<double2*>(smem + (((size_t)8 * n + 15) & ~(size_t)15));
     uint32_t* smeta = reinterpret_cast<uint32_t*>(smin + m);
+    uint32_t* vote = reinterpret_cast<uint32_t*>(smem + ((((size_t)8 * n + 15) & ~(size_t)15) + (size_t)20 * m + 15) / 16 * 16);  // [2][16]
     const double* __restrict__ ch = llr + frame * ld;
     const int32_t* __restrict__ rp = dv.row_ptr;
     const int32_t* __restrict__ ci = dv.col_idx;
@@ -999,7 +1021,7 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
         }
         }
         if (g.early_stop && it > 0) {
-            if (!__syncthreads_or(syn)) { done = it; break; }
+            if (!wg_any(syn != 0, vote, it & 1)) { done = it; break; }
         } else {
             __syncthreads();
         }

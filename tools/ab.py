@@ -15,7 +15,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-CASES = ("enc_1024", "enc_4096", "awgn_1024", "awgn_8192", "lane_2048_l32", "lane_1024_l64", "lane_512_l4", "lane_8192_l8", "lane_1024_l128", "polar_l8_128k", "polar_l32_64k", "polar_4096_128k", "polar_2048", "polar_l16", "polar_sc128", "polar_sc512", "polar_sc2048", "polar_sc4096", "polar_l8", "ldpc_bp", "ldpc_bp_valid", "polar_l32", "polar_4096", "ms_8192", "polar_sc", "polar_sc_def",
+CASES = ("enc_1024", "enc_4096", "awgn_1024", "awgn_8192", "lane_2048_l32", "lane_1024_l64", "lane_512_l4", "lane_8192_l8", "lane_1024_l128", "polar_l8_128k", "polar_l32_64k", "polar_4096_128k", "polar_2048", "polar_l16", "polar_sc128", "polar_sc512", "polar_sc2048", "polar_sc4096", "polar_l8", "ldpc_bp", "ldpc_bp_valid", "polar_l32", "polar_4096", "ms_8192", "ms_8192_es", "ms_504", "polar_sc", "polar_sc_def",
          "polar_sc256")
 
 
@@ -119,6 +119,27 @@ def worker(cases):
             llr = torch.empty((B, n), dtype=torch.float64, device="cuda")
             ms = timeit(lambda: ch.llr_batch_device(cw, n, B, seed=9, out=llr))
             res[case] = dict(ms=ms, digest=int(llr.view(torch.int64).sum().item()))
+        elif case == "ms_8192_es":  # the bench's long_ms key: early stop at 1.5 dB, all-zero codeword
+            from polarcode_and_ldpc_amd.ldpc import MSDecoder
+            from polarcode_and_ldpc_amd.ldpc.matrix import regular_construction
+            H = regular_construction(8192, 3, 6, seed=11)
+            plan = MSDecoder(H, max_iter=20, early_stop=True).plan
+            B = 16384
+            llr = AWGNChannel(1.5).llr_batch_device(None, 8192, B, seed=47)
+            out = torch.empty((B, 8192), dtype=torch.uint8, device="cuda")
+            its = torch.empty((B,), dtype=torch.int32, device="cuda")
+            ms = timeit(lambda: plan.decode(llr, out, its))
+            res[case] = dict(ms=ms, digest=digest(out) ^ digest(its), mean_it=float(its.double().mean().item()))
+        elif case == "ms_504":  # min-sum, (3,6)-regular n=504 (ldpc_reg_kernel; the seed-42 H has degree-1 checks), early stop, 1 dB
+            from polarcode_and_ldpc_amd.ldpc import MSDecoder
+            from polarcode_and_ldpc_amd.ldpc.matrix import regular_construction
+            plan = MSDecoder(regular_construction(504, 3, 6, seed=5), max_iter=20, early_stop=True).plan
+            B = 65536
+            llr = AWGNChannel(1.0).llr_batch_device(None, 504, B, seed=48)
+            out = torch.empty((B, 504), dtype=torch.uint8, device="cuda")
+            its = torch.empty((B,), dtype=torch.int32, device="cuda")
+            ms = timeit(lambda: plan.decode(llr, out, its))
+            res[case] = dict(ms=ms, digest=digest(out) ^ digest(its), mean_it=float(its.double().mean().item()))
         elif case == "ms_8192":
             from polarcode_and_ldpc_amd.ldpc import MSDecoder
             from polarcode_and_ldpc_amd.ldpc.matrix import regular_construction

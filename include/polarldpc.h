@@ -54,12 +54,12 @@ typedef struct {
  *   N power of two (2..32768); K = number of unfrozen positions, 1 <= K <= N
  *   (the reference's 0 < K < N assertion, decoder.py:17-18, is made by the
  *   Python layer on its K argument, exactly as the reference does).
- *   list_size <= 2048: lists above 64 run one frame per workgroup of
- *   list_size/64 wavefronts (16-bit path slots above 256); lists of 1025..2048
- *   run every frame through the exact single-workgroup decoder of
- *   polar_nan.hip (list state in LDS and workspace; milliseconds per frame);
- *   larger lists return PL_EUNSUPPORTED (the reference accepts any L, its
- *   scripts use <= 32).
+ *   list_size: lists above 64 run one frame per workgroup of list_size/64
+ *   wavefronts (16-bit path slots above 256); lists above 1024 run every frame
+ *   through the exact single-workgroup decoder of polar_nan.hip (milliseconds
+ *   per frame; its per-frame list state in LDS up to 2048 paths, in the
+ *   workspace above).  list_size > 65536 or list_size * N > 2^30 returns
+ *   PL_EUNSUPPORTED (the reference accepts any L, its scripts use <= 32).
  *   flags: 0 = fastest kernel built for (N, list size).  Diagnostics: bits 0-3
  *   force the lane kernel (polar_lane.hip) with that fused-top depth, 0x10 or
  *   0x20 the lane kernel with its default depth.

@@ -215,8 +215,8 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
         return fail(PL_EINVAL, "N must be a power of 2 in [2, 32768]");
     if (!(0 < K && K <= N)) return fail(PL_EINVAL, "K (info positions) must be in [1, N]");
     if (list_size < 0) return fail(PL_EINVAL, "list_size must be >= 1 (0 = SC)");
-    if (list_size > pl::kMaxRedoList)
-        return fail(PL_EUNSUPPORTED, "list_size > 2048 not supported by this build (the list state of one frame in LDS)");
+    if (list_size > pl::kMaxListSize || (int64_t)list_size * N > pl::kMaxListTimesN)
+        return fail(PL_EUNSUPPORTED, "list_size > 65536 or list_size * N > 2^30 not supported by this build");
     if (!frozen_mask) return fail(PL_EINVAL, "frozen_mask is NULL");
     int n = 0;
     while ((1 << n) < N) ++n;
@@ -306,7 +306,7 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
         p->mask_bytes = p->generic ? 0 : pl::nan_mask_region(p->lane_grid_max);
         p->redo_unit = pl::nan_redo_unit(N, list_size);
         p->redo_blocks = device_cus(p->device);
-        if (p->generic) {  // scratch of up to 2 GB: a 2048-path list of N = 1024 holds 23 MB per frame
+        if (p->generic) {  // scratch of up to 2 GB (at least one frame's): a 2048-path list of N = 1024 holds 23 MB
             const size_t cap = (size_t)2 << 30;
             p->redo_blocks = (int)std::max<size_t>(1, std::min<size_t>((size_t)p->redo_blocks, cap / p->redo_unit));
             p->lane_grid_max = p->redo_blocks;

@@ -5,9 +5,10 @@
 
 #ifndef PL_METRIC_FUSED_NMAX
 // polar tree instances with n <= this use the fused log1p(exp(-x))
-// (log1p_exp_neg): N=1024 L=8 -1.9 %, L=32 -2.6 %; N=4096 L=8 +3.6 % (register
-// allocation), so larger codes keep log1p_pos(exp_neg(x)) (polar_common.hpp)
-#define PL_METRIC_FUSED_NMAX 10
+// (log1p_exp_neg): N=1024 L=8 -1.9 %, L=32 -2.6 % (round 4); N=4096 L=8 +3.6 %
+// then (register allocation), -0.6 % with round 5's 16 waves per CU and
+// de-duplicated fused top -- every tree instance (n <= 12) now uses it
+#define PL_METRIC_FUSED_NMAX 12
 #endif
 
 namespace pl {
@@ -70,6 +71,10 @@ hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t
 // kNanMaskPasses passes of its persistent grid.
 constexpr int kNanMaskPasses = 64;
 constexpr int kMaxRedoList = 2048;  // the redo kernel's list state of one frame fits LDS up to here
+// lists above kMaxRedoList keep that state in global scratch; list_size * N is
+// bounded so that the kernel's int indices (path x element) stay below 2^31
+constexpr int kMaxListSize = 1 << 16;
+constexpr int64_t kMaxListTimesN = (int64_t)1 << 30;
 // Bytes of the mask words of up to `grid` wavefronts, u64 [grid][kNanMaskPasses]
 // (a multiple of 64 KB, at the start of a list plan's workspace).  They are zero
 // between decodes: zeroed when the workspace is allocated, ORed by the list

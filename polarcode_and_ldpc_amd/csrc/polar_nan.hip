@@ -27,8 +27,12 @@
 // counts: at most one copy per extra child).
 //
 // The same kernel, launched without masks, is the decoder of lists above 1024
-// paths (up to kMaxRedoList; the list kernels hold one lane per path in one
-// workgroup): every frame, one workgroup each.
+// paths (the list kernels hold one lane per path in one workgroup): every
+// frame, one workgroup each.  Up to kMaxRedoList paths the frame's list state
+// (candidates, sort scratch, metrics, buffer tables: lds_frame_bytes) sits in
+// LDS; above that (polar_nan_redo_kernel<true>, lists of up to kMaxListSize
+// paths) it sits in the workgroup's global scratch after the path buffers --
+// the same code on flat pointers, a correctness path like the rest of this file.
 #include <algorithm>
 #include <mutex>
 
@@ -84,7 +88,7 @@ __host__ __device__ inline size_t path_bytes(int N) {
     return (8 * e + e + 2 * (size_t)N + 15) & ~(size_t)15;
 }
 
-// one frame, all threads of the workgroup
+// one frame, all threads of the workgroup; smem = the frame state (LDS or scratch)
 PL_DEV void redo_frame(const RedoArgs& a, int64_t frame, const Bufs& bf, unsigned char* smem) {
     const int N = a.N, n = a.n, L = a.Lsz, tid = threadIdx.x;
     PsItem* cand = reinterpret_cast<PsItem*>(smem);               // [2L]
@@ -269,9 +273,15 @@ PL_DEV void redo_frame(const RedoArgs& a, int64_t frame, const Bufs& bf, unsigne
     __syncthreads();
 }
 
+template <bool GSTATE>
 __global__ void __launch_bounds__(kRedoThreads) polar_nan_redo_kernel(RedoArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Bufs bf{a.scratch + (size_t)blockIdx.x * a.unit, a.N, path_bytes(a.N)};
+    if constexpr (GSTATE) {  // lists above kMaxRedoList: state after the path buffers, every frame here
+        unsigned char* const st = bf.base + (size_t)a.Lsz * bf.pbytes;
+        for (int64_t f = blockIdx.x; f < a.batch; f += gridDim.x) redo_frame(a, f, bf, st);
+        return;
+    }
     // flagged (mask, first frame) pairs of one scan round, after the frame state
     uint64_t* const xw = reinterpret_cast<uint64_t*>(smem + lds_frame_bytes(a.Lsz));
     int* const xn = reinterpret_cast<int*>(xw + 2 * kRedoThreads);
@@ -319,9 +329,13 @@ __global__ void __launch_bounds__(kRedoThreads) polar_nan_redo_kernel(RedoArgs a
 
 }  // namespace
 
-size_t nan_redo_unit(int N, int list_size) { return path_bytes(N) * (size_t)list_size; }
+size_t nan_redo_unit(int N, int list_size) {
+    return path_bytes(N) * (size_t)list_size + (list_size > kMaxRedoList ? lds_frame_bytes(list_size) : 0);
+}
 
-int nan_redo_lds_bytes(int list_size) { return (int)(lds_frame_bytes(list_size) + 16 * kRedoThreads + 16); }
+int nan_redo_lds_bytes(int list_size) {
+    return list_size > kMaxRedoList ? 0 : (int)(lds_frame_bytes(list_size) + 16 * kRedoThreads + 16);
+}
 
 // The kernel's dynamic-LDS limit is a per-function attribute: raise it to what
 // this plan's list needs (never lower it under another plan), per device.
@@ -332,12 +346,13 @@ hipError_t nan_redo_prepare(int list_size) {
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     const int need = nan_redo_lds_bytes(list_size);
+    if (list_size > kMaxRedoList) return hipSuccess;  // state in scratch, no dynamic LDS
     std::lock_guard<std::mutex> lk(mu);
     if (dev >= 0 && dev < 64 && need <= set_bytes[dev]) return hipSuccess;
     int optin = 0;
     if ((e = hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev)) != hipSuccess) return e;
     if (need > optin) return hipErrorInvalidValue;  // this list's state does not fit the device's LDS
-    e = hipFuncSetAttribute((const void*)polar_nan_redo_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, need);
+    e = hipFuncSetAttribute((const void*)polar_nan_redo_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, need);
     if (e == hipSuccess && dev >= 0 && dev < 64) set_bytes[dev] = need;
     return e;
 }
@@ -356,8 +371,13 @@ hipError_t nan_redo_launch(const double* llr, int64_t ld, uint8_t* out, int64_t 
     int blocks = (int)std::min<int64_t>(std::min<int64_t>(want, fit), max_blocks);
     if (blocks < 1) return hipErrorInvalidValue;
     void* args[] = {(void*)&a};
-    return hipLaunchKernel((const void*)polar_nan_redo_kernel, dim3((unsigned)blocks), dim3(kRedoThreads), args,
-                           nan_redo_lds_bytes(Lsz), s);
+    if (Lsz > kMaxRedoList) {
+        if (masks) return hipErrorInvalidValue;  // such lists decode every frame here, never flagged
+        return hipLaunchKernel((const void*)polar_nan_redo_kernel<true>, dim3((unsigned)blocks), dim3(kRedoThreads),
+                               args, 0, s);
+    }
+    return hipLaunchKernel((const void*)polar_nan_redo_kernel<false>, dim3((unsigned)blocks), dim3(kRedoThreads),
+                           args, nan_redo_lds_bytes(Lsz), s);
 }
 
 }  // namespace pl

@@ -76,9 +76,6 @@ namespace {
 #ifndef PL_SC_FUNROLL
 #define PL_SC_FUNROLL 16  // SC instances: unroll of the depth-1 loop over the channel
 #endif
-#ifndef PL_DEDUP_NMAX
-#define PL_DEDUP_NMAX 10  // largest n whose fused top de-duplicates its staged reads
-#endif
 
 // Lane exchanges inside the 8-lane group of a frame (LCAP = 8) without LDS:
 // quad_perm xor 1/2/3 and row_half_mirror (lane i <- 7 - i = i ^ 7 in each
@@ -223,7 +220,11 @@ struct TG {
     static constexpr int L_ROW = L_MET + FPW * GS;                     // [FPW][GS]: (lrow, brow)
     static constexpr int L_BR = L_ROW + FPW * GS;                      // [64] u64: beta registers
     static constexpr int L_SURV = L_BR + 64 * 8;                       // [64] u32: survivor entries
-    static constexpr int L_FINAL = L_MET;                              // [FPW][CW] u32 (aliases scratch)
+    // [FPW][CW] u32: the final transform's words, written once the best path
+    // is known, alias the LDS pools and the pruning scratch (all dead by then).
+    // Before round 5 they sat after the pools, which put n = 12 L = 8 at 11 KB
+    // (14 waves per CU instead of 16) and SC N = 2048 / 4096 at 47 / 63 KB
+    static constexpr int L_FINAL = 0;
     static constexpr int L_END0 = L_SURV + 64 * 4;
     static constexpr int L_END1 = L_FINAL + FPW * CW * 4;
     static constexpr int LDS = (((L_END0 > L_END1) ? L_END0 : L_END1) + 15) & ~15;
@@ -259,10 +260,10 @@ struct TG {
     // fused top from staged depth D0 with de-duplicated chunk reads: a chunk is
     // LCAP pairs of every frame, W / 2 = 2^(F-D0-1) of them per depth-F
     // element, and the depth-F array (2^(n-F) elements) must fill at least one
-    // chunk; n <= 10 only (at N = 2048 / 4096, L = 8 it measured slower, 8.7 /
-    // 13.0 ms against 8.3 / 12.0)
+    // chunk (round 3 measured it slower at N = 2048 / 4096, L = 8; with round
+    // 5's 16 waves per CU and issue priorities at n = 12 it is faster there)
     static constexpr bool dedup(int D0) {
-        return STAGE && n <= PL_DEDUP_NMAX && LCAP >= (1 << (F - D0)) / 2 && (1 << (n - F)) * ((1 << (F - D0)) / 2) >= LCAP;
+        return STAGE && LCAP >= (1 << (F - D0)) / 2 && (1 << (n - F)) * ((1 << (F - D0)) / 2) >= LCAP;
     }
     static PL_DEV int pl(int s, int f) { return SHADOW ? s * FPW + f : f * LCAP + s; }
 };
@@ -413,7 +414,7 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
             // the next chunk's prefetch: unconditional (the last chunk re-reads
             // itself; a conditional one made the compiler's wait for the words
             // above a vmcnt(0) on the path without it, draining the prefetch)
-            constexpr int UNR = G::LCAP == 16 ? 4 : 2;  // element-loop unroll
+            constexpr int UNR = G::LCAP == 16 ? 4 : 2;  // element-loop unroll (4 at L = 32: +20 %)
             auto prefetch = [&]() {
                 const int cn = c + 1 < NCH ? c + 1 : c;
 #pragma unroll
@@ -660,9 +661,9 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
     // (the static b, b + grid, b + 2 grid, ... measured 8.5 % slower at L = 32)
     const int64_t ngrp = (batch + FPW - 1) / FPW;
     unsigned int* const sched = reinterpret_cast<unsigned int*>(workspace - kSchedBytes);
-    // (not at n = 12, whose launches are bound by memory bandwidth: +3 % at
-    // 131 072 frames, profiles/r04_a/ab_prio_4096.log)
-    constexpr int PRIO = G::n <= 11 ? PL_TREE_PRIO : 0;
+    // (at n = 12 with 14 waves per CU it cost 3-5 %, profiles/r04_a/ab_prio_4096.log;
+    // with 16 it gains 2.4 %, profiles/r05_b/ab_t12*.log)
+    constexpr int PRIO = PL_TREE_PRIO;
 #if PL_TREE_PRIO >= 2
     // the first group: later-dispatched wavefronts (younger on their SIMD, so
     // behind in the age-ordered issue arbitration) start at a higher priority
@@ -831,7 +832,7 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 bool kept = false;
                 // (measured: L = 16 / 32 at N = 1024 -4.5 % / -4.7 %, L = 8 at N = 4096 -3.7 %,
                 // L = 8 at N = 1024 +1.8 %: eight frames per wave rarely all stay ordered)
-                if constexpr (LCAP >= PL_ORDERED_PRUNE || (NL >= 12 && LCAP >= 8)) {
+                if constexpr (LCAP >= PL_ORDERED_PRUNE || (NL >= 11 && LCAP >= 8)) {
                     if (nact == LCAP && Lsz == LCAP) kept = ordered_prune<LCAP>(m0, m1, slot, lane);
                 }
                 if (kept) {

@@ -35,7 +35,8 @@ int main() {
     EXPECT(pl_polar_plan_create(1024, 511, mask.data(), 8, 0, &p) == PL_EINVAL);  // mask has 512 info bits
     EXPECT(pl_polar_plan_create(1024, 512, nullptr, 8, 0, &p) == PL_EINVAL);
     EXPECT(pl_polar_plan_create(1024, 512, mask.data(), -1, 0, &p) == PL_EINVAL);
-    EXPECT(pl_polar_plan_create(1024, 512, mask.data(), 2049, 0, &p) == PL_EUNSUPPORTED);  // lists above 2048
+    EXPECT(pl_polar_plan_create(1024, 512, mask.data(), 65537, 0, &p) == PL_EUNSUPPORTED);  // lists above 65536
+    EXPECT(pl_polar_plan_create(32768, 512, mask.data(), 65536, 0, &p) == PL_EUNSUPPORTED);  // L * N > 2^30 (checked before the mask)
     EXPECT(pl_polar_plan_create(1 << 16, 8, mask.data(), 8, 0, &p) == PL_EINVAL);
     EXPECT(std::strlen(pl_last_error()) > 0);
     // a valid plan on a machine without a device: a clean device error, no leak

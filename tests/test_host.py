@@ -36,8 +36,8 @@ def test_plan_create_argument_errors():
     rc = _native.lib.pl_polar_plan_create(100, 50, mask.ctypes.data_as(ctypes.c_void_p), 8, 0, ctypes.byref(h))
     assert rc == _native.PL_EINVAL and b"power of 2" in _native.lib.pl_last_error()
     mask = np.zeros(64, np.uint8)
-    rc = _native.lib.pl_polar_plan_create(64, 32, mask.ctypes.data_as(ctypes.c_void_p), 2049, 0, ctypes.byref(h))
-    assert rc == _native.PL_EUNSUPPORTED  # lists above 2048: the exact decoder's LDS
+    rc = _native.lib.pl_polar_plan_create(64, 32, mask.ctypes.data_as(ctypes.c_void_p), 65537, 0, ctypes.byref(h))
+    assert rc == _native.PL_EUNSUPPORTED  # lists above 65536
     rp = np.array([0, 1], np.int32)
     ci = np.array([3], np.int32)
     rc = _native.lib.pl_ldpc_plan_create(1, 4, rp.ctypes.data_as(ctypes.c_void_p), ci.ctypes.data_as(ctypes.c_void_p),

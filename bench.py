@@ -866,6 +866,8 @@ def compact_line(full, detail_path=None):
     if line["roofline"] is not None:
         line["roofline"]["traffic_source"] = "separate PMC pass (see pmc_note)"
     line["cpu_baseline"] = _cpu_short(full.get("cpu_baseline"), with_sample=True)
+    if full.get("cpu_baseline_note"):
+        line["cpu_baseline_note"] = full["cpu_baseline_note"]
     line["ber"], line["fer"] = _r(full.get("ber")), _r(full.get("fer"))
     keys = {}
     for name in ("end_to_end", "default_frozen_set", "polar_sc_default", "config0_sc_256", "ldpc", "cascl_l32"):
@@ -1030,6 +1032,12 @@ def main():
         if ldp is not None:
             full["ldpc"] = ldp
         full.update(extra)
+        if full["cpu_baseline"] is None:
+            # the contract times the CPU path on rank 0 at N = 1 only: the N = 1
+            # line of the same build carries it (the host cores are shared by the
+            # N ranks here, so a figure taken now would measure contention)
+            full["cpu_baseline_note"] = ("not measured: %s" % ("--skip-cpu" if args.skip_cpu else
+                                         "timed on rank 0 at N = 1 only (see the N = 1 line of this build)"))
         path = write_detail(full, args.detail_out)
         print(json.dumps(compact_line(full, path)), flush=True)
     rt.close()

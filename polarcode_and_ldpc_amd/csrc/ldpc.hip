@@ -604,36 +604,47 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
             if (!__ballot(bad != 0u)) { done = it; break; }
         }
         PL_GSTAMP(1)
+        // the product of slot j over its D_s inputs (one instruction stream per wavefront)
+        auto slot_prod = [&](int j, int& base, int& i) -> double {
+            const int D = __builtin_amdgcn_readfirstlane(meta[j] >> 20);  // the slot's D_s
+            base = meta[j] & 0xFFFF;
+            i = (meta[j] >> 16) & 15;
+            const double* tb = T + base;
+            switch (D) {
+                case 0: return 0.0;  // slot past the last edge (not stored)
+                case 1: return grp_prod<1>(tb, i);
+                case 2: return grp_prod<2>(tb, i);
+                case 3: return grp_prod<3>(tb, i);
+                case 4: return grp_prod<4>(tb, i);
+                case 5: return grp_prod<5>(tb, i);
+                case 6: return grp_prod<6>(tb, i);
+                case 7: return grp_prod<7>(tb, i);
+                case 8: return grp_prod<8>(tb, i);
+                case 9: return grp_prod<9>(tb, i);
+                case 10: return grp_prod<10>(tb, i);
+                case 11: return grp_prod<11>(tb, i);
+                case 12: return grp_prod<12>(tb, i);
+                case 13: return grp_prod<13>(tb, i);
+                case 14: return grp_prod<14>(tb, i);
+                default: return grp_prod<15>(tb, i);
+            }
+        };
+        // clip, 2*atanh, nan_to_num: after the clip 2*atanh is finite, so
+        // only a NaN product (NaN channel LLRs) maps to 0.  (This form -- the
+        // uniform skip of an empty slot ahead of the product, the product as a
+        // function returning from its switch -- schedules 3 % faster than the
+        // same operations written inline, 6.21 -> 6.03 ms, bits identical; two
+        // slots' 2*atanh chains side by side: 6.14, profiles/r05_b/ab_bp_pair.log)
+        auto c2v_of = [](double p) -> double {
+            const double o = two_atanh(__builtin_fmax(__builtin_fmin(p, 0.999999), -0.999999));
+            return __builtin_isnan(p) ? 0.0 : o;
+        };
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
-            const int D = __builtin_amdgcn_readfirstlane(meta[j] >> 20);  // the slot's D_s
-            if (D == 0) continue;                                          // slot past the last edge
-            const int base = meta[j] & 0xFFFF, i = (meta[j] >> 16) & 15;
-            const double* tb = T + base;
-            double p;
-            switch (D) {
-                case 1: p = grp_prod<1>(tb, i); break;
-                case 2: p = grp_prod<2>(tb, i); break;
-                case 3: p = grp_prod<3>(tb, i); break;
-                case 4: p = grp_prod<4>(tb, i); break;
-                case 5: p = grp_prod<5>(tb, i); break;
-                case 6: p = grp_prod<6>(tb, i); break;
-                case 7: p = grp_prod<7>(tb, i); break;
-                case 8: p = grp_prod<8>(tb, i); break;
-                case 9: p = grp_prod<9>(tb, i); break;
-                case 10: p = grp_prod<10>(tb, i); break;
-                case 11: p = grp_prod<11>(tb, i); break;
-                case 12: p = grp_prod<12>(tb, i); break;
-                case 13: p = grp_prod<13>(tb, i); break;
-                case 14: p = grp_prod<14>(tb, i); break;
-                default: p = grp_prod<15>(tb, i); break;
-            }
-            // clip, 2*atanh, nan_to_num: after the clip 2*atanh is finite, so
-            // only a NaN product (NaN channel LLRs) maps to 0
-            const bool pn = __builtin_isnan(p);
-            double o = two_atanh(__builtin_fmax(__builtin_fmin(p, 0.999999), -0.999999));
-            o = pn ? 0.0 : o;
-            C[base + i] = o;  // lanes without an edge: the sink
+            if (__builtin_amdgcn_readfirstlane(meta[j] >> 20) == 0) continue;  // slot past the last edge
+            int base, i;
+            const double p = slot_prod(j, base, i);
+            C[base + i] = c2v_of(p);  // lanes without an edge: the sink
         }
         PL_GSTAMP(2)
         __syncthreads();

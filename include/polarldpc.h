@@ -41,9 +41,10 @@ typedef struct {
     int32_t lds_bytes;  /* dynamic LDS per workgroup of the decode kernel          */
     int32_t fused_top;  /* polar: tree depths fused into the channel read (>=1)    */
     int32_t frames_per_block; /* frames one workgroup decodes                     */
-    int32_t reserved;   /* polar: kernel generation (4 tree, 3 lane);
-                           LDPC: 2 register-cached, 1 generic, 3 thread-per-check,
-                           5 min-sum with compressed check state */
+    int32_t reserved;   /* polar: kernel (4 tree, 3 lane, 6 single-workgroup exact);
+                           LDPC: 2 register-cached, 7 register-cached BP with
+                           degree-grouped check products, 1 generic,
+                           3 thread-per-check, 5 min-sum with compressed check state */
 } pl_plan_info;
 
 /* Polar SC / SCL plan.

@@ -914,9 +914,9 @@ extern "C" int pl_plan_get_info(const pl_plan* p, pl_plan_info* info) {
     } else {
         info->kind = 1; info->n_in = p->lg.n; info->n_out = p->lg.n; info->list_size = 0;
         info->lds_bytes = p->lg.lds_bytes; info->fused_top = 0; info->frames_per_block = 1;
-        // kernel: 2 register-cached, 1 generic (LDS or global workspace), 3 thread-per-check,
-        // 5 min-sum with compressed check state
-        info->reserved = p->lg.compact ? 5 : (p->lg.check_kernel ? 3 : (p->lg.reg_variant ? 2 : 1));
+        // kernel: 2 register-cached, 7 register-cached BP with degree-grouped products,
+        // 1 generic (LDS or global workspace), 3 thread-per-check, 5 min-sum with compressed check state
+        info->reserved = p->lg.compact ? 5 : (p->lg.check_kernel ? 3 : (p->lg.grp ? 7 : (p->lg.reg_variant ? 2 : 1)));
     }
     return PL_OK;
 }

@@ -230,3 +230,32 @@ def test_global_workspace_two_streams(gpu, oracle):
     rp, ci = L.dense_to_csr(H)
     wb, wi = oracle.ldpc_decode(rp, ci, 8192, xs[0][:4].cpu().numpy(), "bp", 8, True, 1.0, threads=4)
     assert np.array_equal(b[:4].cpu().numpy(), wb) and np.array_equal(i[:4].cpu().numpy(), wi)
+
+
+@pytest.mark.parametrize("code,n,dv,dc", [("mackay", 504, 3, 6), ("mackay", 600, 3, 6), ("regular", 1000, 3, 6),
+                                          ("regular", 480, 4, 8), ("regular", 720, 4, 8)])
+def test_bp_grouped_variants_vs_oracle(gpu, oracle, code, n, dv, dc):
+    """BP through ldpc_bp_grp_kernel at its (DV, EPT, VPT) instances (3,6,2),
+    (3,8,2), (3,12,4), (4,8,2), (4,16,4): irregular MacKay codes (check degrees
+    0..15 around dc, so slots mix degrees and the plan pads checks up to their
+    slots' largest degree; n = 600 has a degree-15 check) and regular ones,
+    with and without early stop, bits and iteration counts against the oracle
+    (src/ldpc/decoder.py:62-122,124-202)."""
+    L = _L()
+    H = (L.mackay_construction(n, n // 2, dv, dc, seed=n + dv) if code == "mackay"
+         else L.regular_construction(n, dv, dc, seed=n + dv))
+    rp, ci = L.dense_to_csr(H)
+    degs = np.diff(rp)
+    rng = np.random.RandomState(n * 10 + dv)
+    B = 48
+    snr = rng.uniform(-1.0, 3.0, size=(B, 1))
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
+    llr = 2.0 * (1.0 + sigma * rng.randn(B, n)) / sigma ** 2
+    llr[1, ::5] = 0.0
+    for es in (True, False):
+        dec = L.BPDecoder(H, 20, es)
+        assert degs.max() <= 15 and dec.plan.info.reserved == 7, (n, dv, int(degs.max()))
+        want_b, want_i = oracle.ldpc_decode(rp, ci, n, llr, algo="bp", max_iter=20, early_stop=es, threads=8)
+        got_b, got_i = dec.decode_batch(llr, return_iterations=True)
+        assert np.array_equal(got_b, want_b), (n, dv, es)
+        assert np.array_equal(got_i, want_i), (n, dv, es)

@@ -713,8 +713,10 @@ static RegVariant reg_variant() {
              (void*)ldpc_bp_grp_kernel<DV, EPT, VPT>}};
 }
 static const RegVariant* reg_table(int& count) {
-    static const RegVariant t[] = {reg_variant<3, 6, 2>(), reg_variant<3, 8, 2>(), reg_variant<3, 12, 4>(),
-                                   reg_variant<3, 16, 4>(), reg_variant<4, 8, 2>(), reg_variant<4, 16, 4>()};
+    // E = DV n for a constant variable degree, so (3, 8, 2) and (3, 16, 4) could
+    // never be picked ahead of (3, 6, 2) / (3, 12, 4): not built
+    static const RegVariant t[] = {reg_variant<3, 6, 2>(), reg_variant<3, 12, 4>(), reg_variant<4, 8, 2>(),
+                                   reg_variant<4, 16, 4>()};
     count = (int)(sizeof(t) / sizeof(t[0]));
     return t;
 }

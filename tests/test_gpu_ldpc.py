@@ -235,8 +235,8 @@ def test_global_workspace_two_streams(gpu, oracle):
 @pytest.mark.parametrize("code,n,dv,dc", [("mackay", 504, 3, 6), ("mackay", 600, 3, 6), ("regular", 1000, 3, 6),
                                           ("regular", 480, 4, 8), ("regular", 720, 4, 8)])
 def test_bp_grouped_variants_vs_oracle(gpu, oracle, code, n, dv, dc):
-    """BP through ldpc_bp_grp_kernel at its (DV, EPT, VPT) instances (3,6,2),
-    (3,8,2), (3,12,4), (4,8,2), (4,16,4): irregular MacKay codes (check degrees
+    """BP through ldpc_bp_grp_kernel at each of its (DV, EPT, VPT) instances
+    (3,6,2), (3,12,4), (4,8,2), (4,16,4): irregular MacKay codes (check degrees
     0..15 around dc, so slots mix degrees and the plan pads checks up to their
     slots' largest degree; n = 600 has a degree-15 check) and regular ones,
     with and without early stop, bits and iteration counts against the oracle

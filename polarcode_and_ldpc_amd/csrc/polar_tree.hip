@@ -257,6 +257,32 @@ struct TG {
     // 6.8 ms at N = 1024); there inactive slots keep their own state and planes
     // and the columns are frame-major, as before.
     static constexpr bool SHADOW = LCAP != 16;
+    // Streaming (nt) accesses for the traffic with the longest reuse distance,
+    // so it does not evict the deeper pools' lines from L2 (round 5; A/B on one
+    // box, bits identical, profiles/r05_b/ab_nt*.log, ab_ntr*.log):
+    //   NTD: the g reads of the NTD shallowest workspace pool depths (F ..
+    //        F+NTD-1) as nt loads -- 2 at n = 10, 3 at n >= 11 (4 at n = 12 and
+    //        3 at n = 10 measured slower), none at L = 16 (slower) nor SC;
+    //   NT_ST: at n <= 10 also those depths' stores (at n >= 11 slower);
+    //   PL_NT_CH: the fused top's chunk prefetch (channel rows / staged nodes).
+    // N = 4096 L = 8 61.1 -> 57.8 ms, N = 2048 7.27 -> 6.85, N = 1024 L = 8
+    // 5.53 -> 5.40, L = 32 18.85 -> 17.95.  (Round 2 had found nt stores
+    // slower, before the dynamic group counter and the issue priorities.)
+#ifndef PL_NT_DEPTHS
+#define PL_NT_DEPTHS -1  // -1: the per-instance rule
+#endif
+#ifndef PL_NT_SC
+#define PL_NT_SC 0
+#endif
+    static constexpr int NTD = PL_NT_DEPTHS >= 0 ? PL_NT_DEPTHS
+                               : (LCAP == 1 ? PL_NT_SC : (LCAP == 16 ? 0 : (n >= 11 ? 3 : 2)));
+#ifndef PL_NT_ST
+#define PL_NT_ST -1  // -1: the per-instance rule
+#endif
+#ifndef PL_NT_CH
+#define PL_NT_CH 1
+#endif
+    static constexpr bool NT_ST = PL_NT_ST >= 0 ? PL_NT_ST != 0 : n <= 10;
     // fused top from staged depth D0 with de-duplicated chunk reads: a chunk is
     // LCAP pairs of every frame, W / 2 = 2^(F-D0-1) of them per depth-F
     // element, and the depth-F array (2^(n-F) elements) must fill at least one
@@ -324,7 +350,15 @@ PL_DEV void fold(Fold<G>& st, double v, int idx, unsigned char* smem, unsigned c
     } else {
         if (idx & 1) {
             double2* dst = reinterpret_cast<double2*>((D >= G::DL ? smem : ws) + G::llr_off(D));
-            if (G::DS != 2 || !((st.skip >> D) & 1u)) dst[(idx >> 1) * 64 + plane] = make_double2(st.pend[D], v);
+            if (G::DS != 2 || !((st.skip >> D) & 1u)) {
+                if constexpr (G::NT_ST && D < G::F + G::NTD && D < G::DL) {
+                    double2* a = dst + (idx >> 1) * 64 + plane;
+                    __builtin_nontemporal_store(st.pend[D], &a->x);
+                    __builtin_nontemporal_store(v, &a->y);
+                } else {
+                    dst[(idx >> 1) * 64 + plane] = make_double2(st.pend[D], v);
+                }
+            }
             fold<G, D + 1>(st, f_ms(st.pend[D], v), idx >> 1, smem, ws, plane);
         } else {
             st.pend[D] = v;
@@ -356,7 +390,15 @@ PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int plane, int p
         }
         double2 pr[U];
 #pragma unroll
-        for (int k = 0; k < U; ++k) pr[k] = src[(t0 + k) * 64];
+        for (int k = 0; k < U; ++k) {
+            // the shallowest workspace depths' g reads as streaming loads (TG::NTD)
+            if constexpr (G::NTD > 0 && P < G::F + G::NTD && P < G::DL) {
+                const double2* a = src + (t0 + k) * 64;
+                pr[k] = make_double2(__builtin_nontemporal_load(&a->x), __builtin_nontemporal_load(&a->y));
+            } else {
+                pr[k] = src[(t0 + k) * 64];
+            }
+        }
 #pragma unroll
         for (int k = 0; k < U; ++k)
             fold<G, Q>(st, g_op(pr[k].x, pr[k].y, w >> ((t0 + k) & 31)), t0 + k, smem, ws, plane);
@@ -418,7 +460,14 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
             auto prefetch = [&]() {
                 const int cn = c + 1 < NCH ? c + 1 : c;
 #pragma unroll
-                for (int h = 0; h < CH; ++h) nxt[h] = src[(cn * CH + h) * cstr];
+                for (int h = 0; h < CH; ++h) {
+                    if constexpr (PL_NT_CH) {
+                        const double2* a = src + (cn * CH + h) * cstr;
+                        nxt[h] = make_double2(__builtin_nontemporal_load(&a->x), __builtin_nontemporal_load(&a->y));
+                    } else {
+                        nxt[h] = src[(cn * CH + h) * cstr];
+                    }
+                }
             };
             // no inner loop (IPC <= UNR): issued here.  Otherwise (LCAP >= 16)
             // inside the loop's first iteration: the loop preheader waits

@@ -16,7 +16,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CASES = ("enc_1024", "enc_4096", "awgn_1024", "awgn_8192", "lane_2048_l32", "lane_1024_l64", "lane_512_l4", "lane_8192_l8", "lane_1024_l128", "polar_l8_128k", "polar_l32_64k", "polar_4096_128k", "polar_2048", "polar_l16", "polar_sc128", "polar_sc512", "polar_sc2048", "polar_sc4096", "polar_l8", "ldpc_bp", "ldpc_bp_valid", "polar_l32", "polar_4096", "ms_8192", "ms_8192_es", "ms_504", "polar_sc", "polar_sc_def", "polar_sc_def_128k", "polar_sc_def_256k",
-         "polar_sc256")
+         "polar_sc256", "cascl_l32")
 
 
 def worker(cases):
@@ -76,6 +76,21 @@ def worker(cases):
             out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
             ms = timeit(lambda: plan.decode(llr, out))
             res[case] = dict(ms=ms, digest=digest(out), errors=int((out != msg).any(dim=1).sum().item()))
+        elif case == "cascl_l32":  # the bench's cascl_l32 key: CRC-8 messages, seed 44, 1 dB
+            from polarcode_and_ldpc_amd.polar import CASCLDecoder
+            from polarcode_and_ldpc_amd.polar.utils import CRC_POLYNOMIALS
+            N, K, L, B = 1024, 512, 32, 65536
+            fr = construct_frozen_set(N, K, 2.0)
+            dec = CASCLDecoder(N, K, list_size=L, frozen_bits=fr, crc_polynomial="CRC-8")
+            msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+            _native.random_bits(44, 0, msg)
+            _native.crc_append(msg, K - 8, 8, CRC_POLYNOMIALS["CRC-8"])
+            cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+            _native.polar_encode(dec.plan, msg, cw)
+            llr = AWGNChannel(1.0).llr_batch_device(cw, N, B, seed=44)
+            out = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+            ms = timeit(lambda: dec.plan.decode(llr, out))
+            res[case] = dict(ms=ms, digest=digest(out))
         elif case == "ldpc_bp_valid":
             from polarcode_and_ldpc_amd.ldpc import BPDecoder, LDPCEncoder
             enc = LDPCEncoder(504, 252, dv=3, dc=6, seed=42)

@@ -188,6 +188,10 @@ def roofline(name, kernel, frames, bytes_per_frame, kms):
     r["traffic_frac"] = r["traffic_GBps"] / HBM_PEAK_GBS
     r["traffic_frac_of_achievable"] = r["traffic_GBps"] / HBM_ACHIEVABLE_GBS
     r["traffic_frames_profiled"] = p.get("frames")
+    # the PMC pass's library build against the one measured now (pmc_summary.py records it)
+    from polarcode_and_ldpc_amd import _native
+    r["traffic_build"] = p.get("build")
+    r["traffic_same_build"] = p.get("build") == _native.build_id()
     if "wave_time_shares" in p:
         r["wave_time_shares"] = p["wave_time_shares"]
     cus = torch.cuda.get_device_properties(0).multi_processor_count
@@ -550,8 +554,46 @@ def bench_config0(args, rt, pool):
 
 
 # ---------------------------------------------------------------- LDPC
+LDPC_KERNELS = {1: "ldpc_decode_kernel<BP>", 2: "ldpc_reg_kernel<BP,DV=3>", 3: "ldpc_check_kernel<BP>",
+                5: "ldpc_ms_compact_kernel<8,3,6,true>", 7: "ldpc_bp_grp_kernel<3,6,2,false>"}
+
+
+def ldpc_kernel_name(plan):
+    """The kernel pl_plan_get_info's `reserved` names (capi.cpp pl_plan_get_info)."""
+    return LDPC_KERNELS.get(int(plan.info.reserved), "ldpc kernel id %d" % plan.info.reserved)
+
+
+def bench_ldpc_valid(args, rt, pool, enc, plan, kname):
+    """Second frame source (SURVEY §8 d): valid codewords (all-zero; BP is
+    codeword-symmetric) at the same SNR, early stop on."""
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    n, k, B = enc.n, enc.k, args.batch
+    llr0 = AWGNChannel(args.snr).llr_batch_device(None, n, B, seed=4243, frame_offset=rt.rank * B)
+    out0 = torch.empty((B, n), dtype=torch.uint8, device="cuda")
+    its0 = torch.empty((B,), dtype=torch.int32, device="cuda")
+    vkt = KernelTimer()
+    dt0, pr0 = timed_steps(lambda: vkt(lambda: plan.decode(llr0, out0, its0)), args.steps, args.warmup, rt,
+                           on_timed=vkt.reset)
+    vkms = vkt.mean_ms()
+    res = dict(value=B * rt.world * args.steps * k / dt0 / 1e6, unit="info-Mbps",
+               ms_per_step=dt0 / args.steps * 1e3, kernel_ms=vkms,
+               roofline=roofline("ldpc_bp_504_valid", kname, B, 9 * n, vkms),
+               rank_ms_per_step=[t / args.steps * 1e3 for t in pr0],
+               mean_iterations=float(its0.double().mean().item()),
+               bit_errors=int(out0.sum().item()),
+               what="all-zero codeword frames (device AWGN), BP max_iter=20, early stop")
+    if pool is not None:
+        from oracle import refnumpy as R
+        S = min(args.cpu_frames_numpy, B)
+        lh = llr0[:S].cpu().numpy()
+        res["cpu_baseline"] = numpy_baseline(
+            pool, cpu_processes(), "BP-20 (504,252), all-zero codewords, early stop",
+            lambda: R.ldpc_batch(enc.H, lh, "bp", 20, True, pool=pool)[0], S, k,
+            out0[:S].cpu().numpy().astype(np.int64))
+    return res
+
+
 def bench_ldpc(args, rt, pool):
-    from polarcode_and_ldpc_amd import _native
     from polarcode_and_ldpc_amd.channel import AWGNChannel
     from polarcode_and_ldpc_amd.ldpc import BPDecoder, LDPCEncoder
 
@@ -559,6 +601,9 @@ def bench_ldpc(args, rt, pool):
     enc = LDPCEncoder(n, k, dv=3, dc=6, seed=42)  # throughput_test.py:285 (rank-251 H, direct solving)
     dec = BPDecoder(enc.H, max_iter=20)
     plan = dec.plan
+    kname = ldpc_kernel_name(plan)
+    if "ldpc" not in args.sec:  # a profiling pass of the valid-codeword key alone
+        return dict(valid_codewords=bench_ldpc_valid(args, rt, pool, enc, plan, kname))
     rs = np.random.RandomState(42 + rt.rank)
     U = 4096  # distinct messages, tiled; every frame gets its own noise
     base = enc.encode_batch(rs.randint(0, 2, (U, k)))
@@ -568,8 +613,6 @@ def bench_ldpc(args, rt, pool):
     its = torch.empty((B,), dtype=torch.int32, device="cuda")
     dt, per_rank, kms, c = decode_loop(rt, plan, llr, out, cw, k, args.steps, args.warmup, its)
     counted = rank_fields(per_rank, args.steps, c)
-    kname = {2: "ldpc_reg_kernel<BP,DV=3>", 1: "ldpc_decode_kernel<BP>", 3: "ldpc_check_kernel<BP>"}.get(
-        plan.info.reserved, "?")
     res = dict(metric="decoded info-Mbps, LDPC (504,252) BP max_iter=20, reference-harness frames @ %.1f dB"
                       % args.snr,
                value=B * rt.world * args.steps * k / dt / 1e6, unit="info-Mbps", ms_per_step=dt / args.steps * 1e3,
@@ -578,30 +621,7 @@ def bench_ldpc(args, rt, pool):
                roofline=roofline("ldpc_bp_504", kname, B, 9 * n, kms))
     res["roofline"]["limit"] = "VALU issue (fp64 transcendentals): see roofline.valu"
     if "ldpc_valid" in args.sec:
-        # Second frame source (SURVEY §8 d): valid codewords (all-zero; BP is
-        # codeword-symmetric) at the same SNR, early stop on.
-        llr0 = AWGNChannel(args.snr).llr_batch_device(None, n, B, seed=4243, frame_offset=rt.rank * B)
-        out0, its0 = torch.empty_like(out), torch.empty_like(its)
-        vkt = KernelTimer()
-        dt0, pr0 = timed_steps(lambda: vkt(lambda: plan.decode(llr0, out0, its0)), args.steps, args.warmup, rt,
-                               on_timed=vkt.reset)
-        vkms = vkt.mean_ms()
-        res["valid_codewords"] = dict(value=B * rt.world * args.steps * k / dt0 / 1e6, unit="info-Mbps",
-                                      ms_per_step=dt0 / args.steps * 1e3, kernel_ms=vkms,
-                                      roofline=roofline("ldpc_bp_504_valid", kname, B, 9 * n, vkms),
-                                      rank_ms_per_step=[t / args.steps * 1e3 for t in pr0],
-                                      mean_iterations=float(its0.double().mean().item()),
-                                      bit_errors=int(out0.sum().item()),
-                                      what="all-zero codeword frames (device AWGN), BP max_iter=20, early stop")
-        if pool is not None:
-            from oracle import refnumpy as R
-            S = min(args.cpu_frames_numpy, B)
-            lh = llr0[:S].cpu().numpy()
-            res["valid_codewords"]["cpu_baseline"] = numpy_baseline(
-                pool, cpu_processes(), "BP-20 (504,252), all-zero codewords, early stop",
-                lambda: R.ldpc_batch(enc.H, lh, "bp", 20, True, pool=pool)[0], S, k,
-                out0[:S].cpu().numpy().astype(np.int64))
-        del llr0, out0, its0
+        res["valid_codewords"] = bench_ldpc_valid(args, rt, pool, enc, plan, kname)
     if pool is not None:
         from oracle import oracle as O
         from oracle import refnumpy as R
@@ -740,7 +760,7 @@ def _long_ms(rt, B, steps, es, pool=None):
         value=B * rt.world * steps * k / dt / 1e6, unit="info-Mbps", steps=steps, ms_per_step=dt / steps * 1e3,
         kernel_ms=kms, frames_per_gpu=B, mean_iterations=float(its.double().mean().item()),
         llr_bytes_per_gpu=B * n * 8, fer=float(c[1]) / max(1, c[2]), **rank_fields(pr, steps, c),
-        roofline=roofline("ldpc_ms_8192" + ("" if es else "_noes"), "ldpc_ms_compact_kernel", B, 9 * n, kms))}
+        roofline=roofline("ldpc_ms_8192" + ("" if es else "_noes"), ldpc_kernel_name(dec.plan), B, 9 * n, kms))}
     if pool is not None:
         from oracle import oracle as O
         from oracle import refnumpy as R
@@ -817,7 +837,8 @@ def _roof_short(r):
         return None
     return _r(dict(bound=r.get("bound"), achieved=r.get("achieved"), peak=r.get("peak"), unit=r.get("unit"),
                    frac=r.get("frac"), traffic=r.get("traffic"), kernel=r.get("kernel"),
-                   kernel_ms=r.get("kernel_ms"), frames=r.get("frames_per_launch")))
+                   kernel_ms=r.get("kernel_ms"), frames=r.get("frames_per_launch"),
+                   traffic_same_build=r.get("traffic_same_build")))
 
 
 def _cpu_short(c, with_sample=False):
@@ -1005,7 +1026,7 @@ def main():
         extra["polar_sc_default"] = bench_sc_default(args, rt, pool)
     if "config0" in args.sec:
         extra["config0_sc_256"] = bench_config0(args, rt, pool)
-    ldp = bench_ldpc(args, rt, pool) if "ldpc" in args.sec else None
+    ldp = bench_ldpc(args, rt, pool) if args.sec & {"ldpc", "ldpc_valid"} else None
     if "cascl" in args.sec:
         extra["cascl_l32"] = bench_cascl(args, rt, pool)
     if args.sec & {"long_polar", "long_ms", "long_ms_noes"}:

@@ -61,6 +61,11 @@ typedef struct {
  *   per frame; its per-frame list state in LDS up to 2048 paths, in the
  *   workspace above).  list_size > 65536 or list_size * N > 2^30 returns
  *   PL_EUNSUPPORTED (the reference accepts any L, its scripts use <= 32).
+ *   Cost of the largest lists: one frame's list state takes about
+ *   list_size * N * 11 bytes of workspace (path LLR + bit arrays; 11 GB at
+ *   list_size * N = 2^30, refused when larger than the device's memory), and
+ *   one thread sorts the 2 * list_size candidates of every information bit,
+ *   so such a frame takes seconds to minutes.  Tested up to list_size 4096.
  *   flags: 0 = fastest kernel built for (N, list size).  Diagnostics: bits 0-3
  *   force the lane kernel (polar_lane.hip) with that fused-top depth, 0x10 or
  *   0x20 the lane kernel with its default depth.
@@ -185,6 +190,14 @@ int pl_debug_polar_deadstore(pl_plan* plan, const double* llr_dev, int64_t batch
  * barrier, [7] output.  Timing differs from pl_decode; read shares. */
 int pl_debug_ldpc_stamps(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
                          int32_t* iters_dev, unsigned long long* stamps_dev, void* stream);
+
+/* Test hook, diagnostic build only (the product library returns
+ * PL_EUNSUPPORTED): pl_decode of a list plan that also reports which frames the
+ * list kernel flagged for the exact NaN-order redo decoder (frames with a NaN
+ * input or two inputs of magnitude >= 2^1000 / inf; polar_tree.hip).
+ * flagged_host: `batch` host bytes, 1 = flagged.  Bits are the product path's. */
+int pl_debug_polar_flagged(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
+                           uint8_t* flagged_host, void* stream);
 
 /* Test hook, diagnostic build only (the product library returns
  * PL_EUNSUPPORTED): overwrite the device id a plan is bound to, so the

@@ -25,6 +25,7 @@ EXPORTS = (
     "pl_count_errors", "pl_debug_polar_stamps", "pl_debug_ldpc_stamps", "pl_debug_polar_deadstore", "pl_polar_plan_set_crc", "pl_crc_append",
     "pl_rayleigh_llr", "pl_bsc", "pl_gf2_encode", "pl_decode_ws", "pl_plan_workspace_bytes",
     "pl_plan_release", "pl_plan_workspace_stats", "pl_debug_set_plan_device", "pl_debug_polar_fpw",
+    "pl_debug_polar_flagged",
 )
 
 
@@ -63,6 +64,7 @@ def _load(path=LIB_PATH):
     L.pl_debug_polar_fpw.argtypes = [P, P, I64, I64, P, P, I32, P]
     L.pl_debug_ldpc_stamps.argtypes = [P, P, I64, I64, P, P, P, P]
     L.pl_debug_polar_deadstore.argtypes = [P, P, I64, I64, P, P, I32, P]
+    L.pl_debug_polar_flagged.argtypes = [P, P, I64, I64, P, P, P]
     L.pl_polar_plan_set_crc.argtypes = [P, I32, ctypes.c_uint32]
     L.pl_crc_append.argtypes = [P, I64, I64, I32, I32, ctypes.c_uint32, P]
     L.pl_rayleigh_llr.argtypes = [P, I32, I64, D, ctypes.c_uint64, I64, P, I64, P]

@@ -6,6 +6,6 @@ _ROOT = str(_Path(__file__).resolve().parents[4])
 if _ROOT not in _sys.path:
     _sys.path.insert(0, _ROOT)
 
-from polarcode_and_ldpc_amd.polar.construction import construct_polar_code, bhattacharyya_bounds, construct_frozen_set  # noqa: F401
+from polarcode_and_ldpc_amd.polar.construction import (bhattacharyya_bounds, gaussian_approximation, construct_polar_code, calculate_channel_capacities, construct_frozen_set)  # noqa: F401
 
-__all__ = ['construct_polar_code', 'bhattacharyya_bounds', 'construct_frozen_set']
+__all__ = ['bhattacharyya_bounds', 'gaussian_approximation', 'construct_polar_code', 'calculate_channel_capacities', 'construct_frozen_set']

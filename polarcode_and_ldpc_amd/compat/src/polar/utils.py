@@ -6,6 +6,6 @@ _ROOT = str(_Path(__file__).resolve().parents[4])
 if _ROOT not in _sys.path:
     _sys.path.insert(0, _ROOT)
 
-from polarcode_and_ldpc_amd.polar.utils import bit_reverse, generate_frozen_bits, crc_encode, crc_check, polar_transform  # noqa: F401
+from polarcode_and_ldpc_amd.polar.utils import (bit_reverse, bit_reverse_array, generate_frozen_bits, crc_encode, crc_check, polar_transform_recursive, polar_transform_iterative, polar_transform)  # noqa: F401
 
-__all__ = ['bit_reverse', 'generate_frozen_bits', 'crc_encode', 'crc_check', 'polar_transform']
+__all__ = ['bit_reverse', 'bit_reverse_array', 'generate_frozen_bits', 'crc_encode', 'crc_check', 'polar_transform_recursive', 'polar_transform_iterative', 'polar_transform']

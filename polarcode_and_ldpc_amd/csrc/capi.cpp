@@ -8,6 +8,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <cmath>
 #include <memory>
 #include <mutex>
@@ -307,15 +308,30 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
         p->redo_unit = pl::nan_redo_unit(N, list_size);
         p->redo_blocks = device_cus(p->device);
         if (p->generic) {  // scratch of up to 2 GB (at least one frame's): a 2048-path list of N = 1024 holds 23 MB
+            // one frame's list state must fit the device (list_size * N = 2^30 needs ~11 GB)
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && p->redo_unit > total_b) {
+                pl_plan_destroy(p);
+                return fail(PL_EUNSUPPORTED, "list_size: one frame's list state exceeds this device's memory");
+            }
             const size_t cap = (size_t)2 << 30;
             p->redo_blocks = (int)std::max<size_t>(1, std::min<size_t>((size_t)p->redo_blocks, cap / p->redo_unit));
             p->lane_grid_max = p->redo_blocks;
         }
-        // the redo kernel's dynamic-LDS limit (a per-function attribute) raised to this list's need
+        // the redo kernel's dynamic-LDS limit (a per-function attribute) raised to this list's need;
+        // a list whose state does not fit the device's LDS is refused here, so that any error
+        // of the prepare call itself is a HIP error
+        int optin = 0;
+        if ((e = hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, p->device)) != hipSuccess) {
+            pl_plan_destroy(p);
+            return hipfail(e, "device attribute query");
+        }
+        if (pl::nan_redo_lds_bytes(list_size) > optin) {
+            pl_plan_destroy(p);
+            return fail(PL_EUNSUPPORTED, "list_size: the redo kernel's list state exceeds this device's LDS");
+        }
         if ((e = pl::nan_redo_prepare(list_size)) != hipSuccess) {
             pl_plan_destroy(p);
-            if (e == hipErrorInvalidValue)
-                return fail(PL_EUNSUPPORTED, "list_size: the redo kernel's list state exceeds this device's LDS");
             return hipfail(e, "NaN redo kernel prepare");
         }
     }
@@ -567,10 +583,22 @@ static size_t ws_need(const pl_plan* p, int64_t batch) {
     return p->ws_unit * (size_t)std::min<int64_t>(batch, p->ldpc_chunk);
 }
 
+// Diagnostic-build options of one decode call (none in the product entry points):
+// stamps = the tree kernel's stamp buffer (or, with ds_mode 1 / 2, the dead-store
+// record / replay bitmask); flagged = a host array of `batch` bytes that receives,
+// per frame, whether the list kernel flagged it for the NaN-order redo decoder.
+struct DecodeDiag {
+    unsigned long long* stamps = nullptr;
+    int ds_mode = 0;
+    uint8_t* flagged = nullptr;
+};
+
 // Decode with an explicit workspace of ws_bytes (>= one unit when one is needed):
 // the polar grid / LDPC chunk is clamped to what the workspace holds.
 static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits, int32_t* iters,
-                       void* ws, size_t ws_bytes, unsigned long long* stamps, hipStream_t s, bool zero_masks = false) {
+                       void* ws, size_t ws_bytes, hipStream_t s, bool zero_masks = false,
+                       const DecodeDiag& dg = DecodeDiag()) {
+    unsigned long long* const stamps = dg.stamps;
     const size_t wmin = ws_min(p);
     if (wmin > 0 && (ws == nullptr || ws_bytes < wmin))
         return fail(PL_EINVAL, "workspace smaller than one unit (pl_plan_workspace_bytes)");
@@ -604,11 +632,25 @@ static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld,
             if (p->tree)
                 e = pl::tree_launch(p->tinfo, l0, ld, o0, p->d_frozen_dec, p->d_info_pos, nb, p->pg.K,
                                     p->sc ? 1 : p->list_size, slices, (int)grid, stamps, p->d_crc_g,
-                                    p->sc ? (const void*)p->d_r0k : (const void*)masks, s);
+                                    p->sc ? (const void*)p->d_r0k : (const void*)masks, s, dg.ds_mode);
             else
                 e = pl::lane_launch(p->lgeo, p->sc, l0, ld, o0, p->d_frozen_dec, p->d_info_pos, nb, slices, (int)grid,
                                     p->d_crc_g, masks, s);
             if (e != hipSuccess) return hipfail(e, "polar decode launch");
+            if (masks && dg.flagged) {  // diagnostic: which frames of this pass group were flagged
+                std::vector<uint64_t> mw((size_t)grid * pl::kNanMaskPasses);
+                e = hipMemcpyAsync(mw.data(), masks, mw.size() * 8, hipMemcpyDeviceToHost, s);
+                if (e == hipSuccess) e = hipStreamSynchronize(s);
+                if (e != hipSuccess) return hipfail(e, "NaN mask readback");
+                // word [w][ps] bit f = frame (ps * grid + w) * fpw + f (polar_tree.hip, polar_nan.hip)
+                for (int64_t w = 0; w < grid; ++w)
+                    for (int ps = 0; ps < pl::kNanMaskPasses; ++ps)
+                        for (int f = 0; f < 64; ++f)
+                            if ((mw[(size_t)w * pl::kNanMaskPasses + ps] >> f) & 1) {
+                                const int64_t fr = ((int64_t)ps * grid + w) * p->fpw + f;
+                                if (fr < nb) dg.flagged[b0 + fr] = 1;
+                            }
+            }
             if (masks) {
                 // frames whose list saw a NaN metric, in the reference's candidate order
                 e = pl::nan_redo_launch(l0, ld, o0, nb, p->pg.N, p->pg.K, p->list_size, p->d_frozen_dec,
@@ -774,11 +816,11 @@ extern "C" int pl_decode(pl_plan* p, const double* llr, int64_t batch, int64_t l
     if ((rc = check_device(p))) return rc;
     const hipStream_t s = (hipStream_t)stream;
     const size_t need = ws_need(p, batch);
-    if (!need) return decode_impl(p, llr, batch, ld, bits, iters, nullptr, 0, nullptr, s);
+    if (!need) return decode_impl(p, llr, batch, ld, bits, iters, nullptr, 0, s);
     std::shared_ptr<Workspace> w = stream_entry(p, s);
     std::lock_guard<std::mutex> lk(w->mu);
     if ((rc = grow_ws(p, w.get(), s, need, false))) return rc;
-    return decode_impl(p, llr, batch, ld, bits, iters, w->ptr, w->bytes, nullptr, s);
+    return decode_impl(p, llr, batch, ld, bits, iters, w->ptr, w->bytes, s);
 }
 
 extern "C" int pl_decode_ws(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
@@ -787,8 +829,8 @@ extern "C" int pl_decode_ws(pl_plan* p, const double* llr, int64_t batch, int64_
     if (rc || batch == 0) return rc;
     if (workspace_bytes < 0) return fail(PL_EINVAL, "workspace_bytes < 0");
     if ((rc = check_device(p))) return rc;
-    return decode_impl(p, llr, batch, ld, bits, iters, workspace, (size_t)workspace_bytes, nullptr,
-                       (hipStream_t)stream, true);
+    return decode_impl(p, llr, batch, ld, bits, iters, workspace, (size_t)workspace_bytes, (hipStream_t)stream,
+                       true);
 }
 
 extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
@@ -805,7 +847,9 @@ extern "C" int pl_debug_polar_stamps(pl_plan* p, const double* llr, int64_t batc
     std::shared_ptr<Workspace> w = stream_entry(p, s);
     std::lock_guard<std::mutex> lk(w->mu);
     if ((rc = grow_ws(p, w.get(), s, ws_need(p, batch), false))) return rc;
-    return decode_impl(p, llr, batch, ld, bits, nullptr, w->ptr, w->bytes, stamps_dev, s);
+    DecodeDiag dg;
+    dg.stamps = stamps_dev;
+    return decode_impl(p, llr, batch, ld, bits, nullptr, w->ptr, w->bytes, s, false, dg);
 #endif
 }
 
@@ -824,10 +868,35 @@ extern "C" int pl_debug_polar_deadstore(pl_plan* p, const double* llr, int64_t b
     std::shared_ptr<Workspace> w = stream_entry(p, s);
     std::lock_guard<std::mutex> lk(w->mu);
     if ((rc = grow_ws(p, w.get(), s, ws_need(p, batch), false))) return rc;
-    pl::g_tree_ds_mode = mode;
-    rc = decode_impl(p, llr, batch, ld, bits, nullptr, w->ptr, w->bytes, reinterpret_cast<unsigned long long*>(mask_dev), s);
-    pl::g_tree_ds_mode = 0;
-    return rc;
+    DecodeDiag dg;
+    dg.stamps = reinterpret_cast<unsigned long long*>(mask_dev);
+    dg.ds_mode = mode;
+    return decode_impl(p, llr, batch, ld, bits, nullptr, w->ptr, w->bytes, s, false, dg);
+#endif
+}
+
+// Diagnostic build: an ordinary list decode that also reports, per frame, whether
+// the list kernel flagged it for the NaN-order redo decoder (flagged_host: `batch`
+// bytes, 1 = flagged).  The decode itself is the product path, bits included.
+extern "C" int pl_debug_polar_flagged(pl_plan* p, const double* llr, int64_t batch, int64_t ld, uint8_t* bits,
+                                      uint8_t* flagged_host, void* stream) {
+    if (!p || p->kind != 0 || !flagged_host) return fail(PL_EINVAL, "polar plan and flag array required");
+#if !PL_DIAG
+    (void)llr; (void)batch; (void)ld; (void)bits; (void)stream;
+    return fail(PL_EUNSUPPORTED, "test hook: diagnostic build only (make DIAG=1)");
+#else
+    int rc = check_decode_args(p, batch, ld, llr, bits);
+    if (rc || batch == 0) return rc;
+    if ((rc = check_device(p))) return rc;
+    if (p->generic || p->mask_bytes == 0) return fail(PL_EUNSUPPORTED, "plan has no NaN masks (SC or generic list plan)");
+    std::memset(flagged_host, 0, (size_t)batch);
+    const hipStream_t s = (hipStream_t)stream;
+    std::shared_ptr<Workspace> w = stream_entry(p, s);
+    std::lock_guard<std::mutex> lk(w->mu);
+    if ((rc = grow_ws(p, w.get(), s, ws_need(p, batch), false))) return rc;
+    DecodeDiag dg;
+    dg.flagged = flagged_host;
+    return decode_impl(p, llr, batch, ld, bits, nullptr, w->ptr, w->bytes, s, false, dg);
 #endif
 }
 

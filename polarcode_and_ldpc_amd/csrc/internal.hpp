@@ -53,9 +53,6 @@ struct TreeInfo {
     int F, DL, fpw;
 };
 bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info);
-#if PL_DIAG
-extern int g_tree_ds_mode;  // 1 / 2: tree_launch runs the dead-store record / replay instance
-#endif
 // The tree and lane kernels' frame groups (FPW frames) past the first one per
 // wavefront come from a u32 counter in the kSchedBytes just before their
 // slices (polar_tree.hip, polar_lane.hpp); tree_launch / lane_launch zero it.
@@ -63,7 +60,8 @@ constexpr int kSchedBytes = 4096;
 hipError_t tree_prepare(const TreeInfo& t, int* max_blocks_per_cu);
 hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t* out, const uint32_t* frozen_dec,
                        const int32_t* info_pos, int64_t batch, int K, int Lsz, unsigned char* ws, int grid,
-                       unsigned long long* stamps, const uint32_t* crc_g, const void* aux, hipStream_t s);
+                       unsigned long long* stamps, const uint32_t* crc_g, const void* aux, hipStream_t s,
+                       int ds_mode = 0);  // ds_mode 1 / 2 (PL_DIAG): the dead-store record / replay instance
 
 // SCL frames with NaN path metrics (polar_nan.hip): the list kernels set bit f
 // of masks[wave][pass] for frame f of that pass; polar_nan_redo_kernel decodes

@@ -1358,10 +1358,6 @@ const TreeEntry* tree_table(int* count) {
 
 }  // namespace
 
-#if PL_DIAG
-int g_tree_ds_mode = 0;
-#endif
-
 bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info) {
     int cnt = 0;
     const TreeEntry* t = tree_table(&cnt);
@@ -1405,18 +1401,21 @@ hipError_t tree_prepare(const TreeInfo& t, int* max_blocks_per_cu) {
 
 hipError_t tree_launch(const TreeInfo& t, const double* llr, int64_t ld, uint8_t* out, const uint32_t* frozen_dec,
                        const int32_t* info_pos, int64_t batch, int K, int Lsz, unsigned char* ws, int grid,
-                       unsigned long long* stamps, const uint32_t* crc_g, const void* aux, hipStream_t s) {
+                       unsigned long long* stamps, const uint32_t* crc_g, const void* aux, hipStream_t s,
+                       int ds_mode) {
     void* args[] = {(void*)&llr, (void*)&ld, (void*)&out, (void*)&frozen_dec, (void*)&info_pos, (void*)&batch,
                     (void*)&K,   (void*)&Lsz, (void*)&ws, (void*)&stamps,     (void*)&crc_g,    (void*)&aux};
     void* fn = stamps ? t.fn_stamps : t.fn;
 #if PL_DIAG
-    if (g_tree_ds_mode) {  // pl_debug_polar_deadstore: `stamps` is the record / replay bitmask
-        fn = t.fn_ds[g_tree_ds_mode - 1];
+    if (ds_mode) {  // pl_debug_polar_deadstore: `stamps` is the record / replay bitmask
+        fn = t.fn_ds[ds_mode - 1];
         if (!fn || !stamps) return hipErrorInvalidValue;
         if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, t.lds_bytes);
             e != hipSuccess)
             return e;
     }
+#else
+    if (ds_mode) return hipErrorInvalidValue;
 #endif
     if (!fn) return hipErrorInvalidValue;
     // the frame-group counter (kernel: group loop)

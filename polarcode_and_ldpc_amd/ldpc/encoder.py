@@ -135,6 +135,8 @@ class LDPCEncoder:
             self.H = H
             assert H.shape[1] == n, f"H matrix must have {n} columns"
             self.m = H.shape[0]
+            if n - self.m != k:  # encoder.py:50-51
+                print(f"Warning: H implies k={n - self.m}, but k={k} was provided")
         if G is not None:
             if G.shape == (n, k):
                 self.G = G.T
@@ -189,5 +191,26 @@ class LDPCEncoder:
         _native.gf2_encode(self._g_dev, self.k, self.n, msg, cw)
         return cw
 
+    def _encode_direct(self, message: np.ndarray) -> np.ndarray:
+        """One message through the direct-solving fallback (encoder.py:97-131)."""
+        msg = np.asarray(message, dtype=np.int64) & 1
+        syn = (np.asarray(self.H[:, :self.k]) @ msg) % 2
+        return np.concatenate([msg, self._solve_gf2(np.asarray(self.H[:, self.k:]), syn)])
+
+    def _solve_gf2(self, A: np.ndarray, b: np.ndarray) -> np.ndarray:
+        """A x = b over GF(2) as the reference solves it (encoder.py:133-187)."""
+        return _solve_gf2_batch(np.asarray(A), np.asarray(b).reshape(-1, 1))[:, 0]
+
     def verify_codeword(self, codeword: np.ndarray) -> bool:
         return bool(np.all((self.H @ codeword) % 2 == 0))
+
+    def get_code_rate(self) -> float:
+        """k / n (encoder.py:202-204)."""
+        return self.k / self.n
+
+    def get_parity_check_matrix(self) -> np.ndarray:
+        """A copy of H (encoder.py:206-208)."""
+        return self.H.copy()
+
+    def __repr__(self) -> str:
+        return f"LDPCEncoder(n={self.n}, k={self.k}, rate={self.get_code_rate():.3f})"

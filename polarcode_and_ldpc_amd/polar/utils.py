@@ -87,4 +87,33 @@ def polar_transform(u: np.ndarray) -> np.ndarray:
     return x
 
 
-polar_transform_iterative = polar_transform
+def polar_transform_iterative(u: np.ndarray) -> np.ndarray:
+    """The reference's single-vector transform (src/polar/utils.py:193-229):
+    stage by stage x[i] = (x[i] + x[i+s]) % 2 on a copy of u, so u's dtype is
+    kept and the entries that are never a left operand are not reduced mod 2
+    (identical to polar_transform for 0/1 input)."""
+    x = np.array(u, copy=True)
+    N = len(x)
+    s = 1
+    while s < N:
+        v = x.reshape(N // (2 * s), 2, s)
+        v[:, 0, :] = (v[:, 0, :] + v[:, 1, :]) % 2
+        s *= 2
+    return x
+
+
+def polar_transform_recursive(u: np.ndarray) -> np.ndarray:
+    """The reference's recursive form (src/polar/utils.py:166-190):
+    T(u) = [T((u1 + u2) % 2), T(u2)] over the halves u1, u2 -- evaluated top
+    down (the widest butterfly first), so it returns the same values, dtype
+    and unreduced entries as the recursion; a length-1 u is returned as is."""
+    N = len(u)
+    if N == 1:
+        return u
+    x = np.array(u, copy=True)
+    h = N // 2
+    while h >= 1:
+        v = x.reshape(N // (2 * h), 2, h)
+        v[:, 0, :] = (v[:, 0, :] + v[:, 1, :]) % 2
+        h //= 2
+    return x

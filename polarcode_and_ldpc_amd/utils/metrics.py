@@ -6,9 +6,7 @@ time one batched call when the object has `decode_batch` / `encode_batch`
 (the GPU path of this package)."""
 from __future__ import annotations
 
-import math
 import time
-from statistics import NormalDist
 from typing import Dict, List, Tuple
 
 import numpy as np
@@ -68,15 +66,18 @@ def measure_decoding_throughput(decoder, llr_inputs: List[np.ndarray]) -> Dict[s
 
 def calculate_ber_with_confidence(bit_errors: int, total_bits: int,
                                   confidence: float = 0.95) -> Tuple[float, float, float]:
-    """(BER, lower, upper) Wilson score interval (metrics.py:138-167)."""
+    """(BER, lower, upper) Wilson score interval (metrics.py:138-167), with the
+    reference's quantile (scipy's norm.ppf) and rounding (z ** 2 through pow)."""
     if total_bits == 0:
         return 0.0, 0.0, 0.0
+    from scipy.stats import norm
     p = bit_errors / total_bits
-    z = NormalDist().inv_cdf(1 - (1 - confidence) / 2)
-    den = 1 + z * z / total_bits
-    mid = (p + z * z / (2 * total_bits)) / den
-    half = z * math.sqrt(p * (1 - p) / total_bits + z * z / (4 * total_bits * total_bits)) / den
-    return p, max(0.0, mid - half), min(1.0, mid + half)
+    z = norm.ppf(1 - (1 - confidence) / 2)
+    z2 = z ** 2
+    den = 1 + z2 / total_bits
+    mid = (p + z2 / (2 * total_bits)) / den
+    half = z * np.sqrt(p * (1 - p) / total_bits + z2 / (4 * total_bits ** 2)) / den
+    return p, max(0, mid - half), min(1, mid + half)
 
 
 def calculate_snr_from_ebn0(ebn0_db: float, code_rate: float) -> float:

@@ -33,6 +33,9 @@ Fixture inventory:
   crc.npz              F9  crc_encode vectors for CRC-8/16/24.
   polar_nan.npz        (round 4) SCL frames with NaN path metrics (+-inf / NaN
                            LLRs): CPython's list.sort order of NaN keys.
+  polar_single_inf.npz (round 6) SCL frames with exactly one +-inf / huge input.
+  host_api.npz         (round 6) every exported host function / method's
+                           outputs + the reference's public name inventory.
 """
 import argparse
 import json
@@ -560,9 +563,203 @@ def job_scl_l2048():
     return "polar_scl_l2048.npz", out
 
 
+def single_extreme_frames(N, fr, llr, rng):
+    """Round 6: frames with exactly ONE infinite or huge
+    channel LLR, the case the tree kernel keeps on its fast path (no g can meet
+    two infinities, so no NaN metric; paths can still reach -inf metrics and tie
+    there).  Kinds cycle with the frame index: the value, the sign relative to
+    the noisy LLR it replaces (+1 agrees, -1 contradicts) and the erasure
+    fraction (LLR 0) added around it.  The channel position alternates between
+    an index of the frozen set and one of the information set."""
+    kinds = [(np.inf, +1, 0.0), (np.inf, -1, 0.0), (1e300, -1, 0.0), (1.5e308, +1, 0.0),
+             (np.inf, +1, 0.2), (np.inf, -1, 0.4), (1e300, +1, 0.3), (1.5e308, -1, 0.25)]
+    info = np.setdiff1d(np.arange(N), fr)
+    out = llr.copy()
+    pos = np.zeros(len(llr), np.int64)
+    for f in range(len(llr)):
+        val, rel, er = kinds[f % len(kinds)]
+        x = out[f]
+        if er:
+            x[rng.rand(N) < er] = 0.0
+        p = int(rng.choice(fr if (f // len(kinds)) % 2 == 0 else info))
+        s = 1.0 if x[p] >= 0 else -1.0
+        x[p] = s * rel * val
+        pos[f] = p
+    return out, pos
+
+
+def job_polar_single_inf():
+    """Reference SCL decodes of single-extreme-input frames (single_extreme_frames):
+    N=1024 K=512 at L=8 and L=32 (16 frames each, the same frames), N=2048 K=1024
+    and N=4096 K=2048 at L=8 (8 frames each), 1 dB, bit-reversed Bhattacharyya sets.
+    Semantics: decoder.py:306-307 (stable sort of -inf ties), :374-406 (metrics
+    of +-inf LLRs), :412-417 (g with one infinite operand)."""
+    polar, _, _ = _imp()
+    out = {}
+    for N, K, Ls, nfr in ((1024, 512, (8, 32), 16), (2048, 1024, (8,), 8), (4096, 2048, (8,), 8)):
+        fr = bitrev_bhatta_frozen(N, K)
+        llr, msg, _ = _polar_frames(N, K, fr, (1.0,), nfr, 1600 + N // 256)
+        llr, pos = single_extreme_frames(N, fr, llr, np.random.RandomState(1700 + N // 256))
+        out["N%d_frozen" % N] = fr
+        out["N%d_llr" % N] = llr
+        out["N%d_msg" % N] = msg
+        out["N%d_pos" % N] = pos
+        out["N%d_Ls" % N] = np.array(Ls)
+        for L in Ls:
+            d = polar.SCLDecoder(N, K, list_size=L, frozen_bits=fr)
+            out["N%d_L%d" % (N, L)] = np.array([d.decode(l.copy()) for l in llr])
+    return "polar_single_inf.npz", out
+
+
+def _public_names():
+    """{module: [public top-level names]} and {module.Class: [public methods]}
+    of the reference's src/ packages, read from the files' syntax trees."""
+    import ast
+    mods, meths = {}, {}
+    src = os.path.join(REF, "src")
+    for pkg in ("polar", "ldpc", "channel", "utils", "lib_wrappers"):
+        for f in sorted(os.listdir(os.path.join(src, pkg))):
+            if not f.endswith(".py") or f == "__init__.py":
+                continue
+            tree = ast.parse(open(os.path.join(src, pkg, f), encoding="utf-8").read())
+            mod = "%s.%s" % (pkg, f[:-3])
+            mods[mod] = [n.name for n in tree.body
+                         if isinstance(n, (ast.FunctionDef, ast.ClassDef)) and not n.name.startswith("_")]
+            for n in tree.body:
+                if isinstance(n, ast.ClassDef):
+                    meths[mod + "." + n.name] = [m.name for m in n.body
+                                                 if isinstance(m, ast.FunctionDef) and not m.name.startswith("_")]
+    return mods, meths
+
+
+def job_host_api():
+    """Round 6: outputs of every host-side function and
+    method the reference's packages export (construction incl. the GA and
+    default methods, transforms, CRC, encoders, H builders, Tanner graph,
+    syndrome, channels with seeds, metrics), plus the public name inventory,
+    so tests/test_host_api.py can check the drop-in modules name by name."""
+    polar, ldpc, channel = _imp()
+    import polar.construction as PC
+    import polar.utils as PU
+    import ldpc.matrix as LM
+    import ldpc.utils as LU
+    import utils.metrics as UM
+    out = {}
+    mods, meths = _public_names()
+    out["names_json"] = np.array(json.dumps({"modules": mods, "methods": meths}))
+    # polar construction: all three methods over sizes, rates and design SNRs
+    for N in (8, 16, 64, 256, 1024, 4096):
+        for K in sorted({1, N // 4, N // 2, (3 * N) // 4, N - 1}):
+            for snr in (-2.0, 0.0, 2.0, 5.0):
+                for meth in ("bhattacharyya", "gaussian_approximation", "default"):
+                    fr, info = PC.construct_polar_code(N, K, meth, snr)
+                    key = "cpc_%d_%d_%g_%s" % (N, K, snr, meth)
+                    out[key + "_frozen"], out[key + "_info"] = fr, info
+        for snr in (-2.0, 0.0, 3.0, 6.0):
+            out["bb_%d_%g" % (N, snr)] = PC.bhattacharyya_bounds(N, snr)
+            out["ga_%d_%g" % (N, snr)] = PC.gaussian_approximation(N, snr)
+            out["cap_%d_%g" % (N, snr)] = PC.calculate_channel_capacities(N, snr)
+    # polar utils
+    rng = np.random.RandomState(606)
+    for n in (0, 1, 3, 10):
+        out["brev_%d" % n] = np.array([PU.bit_reverse(i, n) for i in range(1 << n)])
+        arr = rng.randn(1 << n)
+        out["brevarr_%d_in" % n], out["brevarr_%d" % n] = arr, PU.bit_reverse_array(arr, n)
+    for N, K in ((16, 8), (64, 20), (256, 128)):
+        cp = rng.rand(N)
+        fr, info = PU.generate_frozen_bits(N, K, cp)
+        out["gfb_cp_%d_%d_in" % (N, K)], out["gfb_cp_%d_%d_frozen" % (N, K)] = cp, fr
+        out["gfb_cp_%d_%d_info" % (N, K)] = info
+        fr, info = PU.generate_frozen_bits(N, K)
+        out["gfb_%d_%d_frozen" % (N, K)], out["gfb_%d_%d_info" % (N, K)] = fr, info
+    for N in (1, 2, 16, 128):
+        for tag, u in (("bin", rng.randint(0, 2, N)), ("int", rng.randint(0, 5, N)),
+                       ("flt", rng.randint(0, 2, N).astype(float))):
+            out["pt_%d_%s_in" % (N, tag)] = u
+            out["ptr_%d_%s" % (N, tag)] = PU.polar_transform_recursive(u.copy())
+            out["pti_%d_%s" % (N, tag)] = PU.polar_transform_iterative(u.copy())
+    # polar encoder, with and without CRC
+    for N, K, crc, poly in ((16, 8, False, "CRC-8"), (64, 32, True, "CRC-8"), (256, 128, True, "CRC-16"),
+                            (1024, 512, True, "CRC-24"), (128, 40, False, "CRC-8")):
+        enc = polar.PolarEncoder(N, K, use_crc=crc, crc_polynomial=poly)
+        msgs = rng.randint(0, 2, (4, enc.K_data))
+        key = "penc_%d_%d_%d_%s" % (N, K, int(crc), poly)
+        out[key + "_msg"] = msgs
+        out[key + "_cw"] = np.array([enc.encode(m) for m in msgs])
+        out[key + "_info"] = np.asarray(enc.get_info_bits_positions())
+        out[key + "_frozen"] = np.asarray(enc.get_frozen_bits_positions())
+        out[key + "_rate"] = np.array(enc.get_code_rate())
+    # LDPC matrices, encoder, utils
+    for (n, k, dv, dc, seed) in ((504, 252, 3, 6, 42), (96, 48, 3, 6, 7), (120, 60, 3, 6, None), (60, 20, 2, 3, 3)):
+        key = "ldpc_%d_%d_%d_%d_%s" % (n, k, dv, dc, seed)
+        np.random.seed(1234)
+        H = LM.generate_ldpc_matrix(n, k, "mackay", dv, dc, seed)
+        out[key + "_H"] = H
+        np.random.seed(1234)
+        enc = ldpc.LDPCEncoder(n, k, dv=dv, dc=dc, seed=seed)
+        out[key + "_encH"] = enc.get_parity_check_matrix()
+        out[key + "_rate"] = np.array(enc.get_code_rate())
+        out[key + "_direct"] = np.array(enc.use_direct_solving)
+        msgs = rng.randint(0, 2, (6, k))
+        cws = np.array([enc.encode(m) for m in msgs])
+        out[key + "_msg"], out[key + "_cw"] = msgs, cws
+        out[key + "_valid"] = np.array([bool(enc.verify_codeword(c)) for c in cws])
+        G, P = LM.create_systematic_generator(enc.H)
+        out[key + "_hasG"] = np.array(G is not None)
+        if G is not None:
+            out[key + "_G"] = G
+        out[key + "_rank"] = np.array(LM.check_matrix_rank(enc.H))
+        out[key + "_girth"] = np.array(LM.calculate_girth(enc.H))
+        cn, vn = LU.create_tanner_graph(enc.H)
+        out[key + "_tanner_c"] = np.array(json.dumps([list(map(int, c)) for c in cn]))
+        out[key + "_tanner_v"] = np.array(json.dumps([list(map(int, v)) for v in vn]))
+        rx = cws ^ (rng.rand(*cws.shape) < 0.03)
+        out[key + "_rx"] = rx
+        out[key + "_syn"] = np.array([LU.calculate_syndrome(enc.H, r) for r in rx])
+        out[key + "_synok"] = np.array([bool(LU.check_syndrome(enc.H, r)) for r in rx])
+        out[key + "_errs"] = np.array([LU.count_errors(c, r) for c, r in zip(cws, rx)])
+        out[key + "_ham"] = np.array([LU.hamming_distance(c, r) for c, r in zip(cws, rx)])
+    for (n, k, dv) in ((24, 12, 3), (60, 30, 2), (50, 10, 4)):
+        out["peg_%d_%d_%d" % (n, k, dv)] = LM.peg_construction(n, k, dv)
+    np.random.seed(77)
+    out["ldpc_random_H"] = LM.generate_ldpc_matrix(40, 20, "random", seed=5)
+    # channels (seeded: the global legacy stream)
+    bits = rng.randint(0, 2, 200)
+    out["ch_bits"] = bits
+    for snr in (-1.0, 0.0, 2.5):
+        ch = channel.AWGNChannel(snr, seed=11)
+        out["awgn_%g_llr" % snr] = ch.transmit(bits, return_llr=True)
+        out["awgn_%g_sym" % snr] = ch.transmit(bits, return_llr=False)
+        out["awgn_%g_mod" % snr] = ch.modulate_bpsk(bits)
+        out["awgn_%g_hard" % snr] = ch.demodulate_bpsk_hard(ch.add_noise(ch.modulate_bpsk(bits)))
+        out["awgn_%g_cap" % snr] = np.array(ch.get_capacity())
+        out["awgn_%g_sigma" % snr] = np.array(ch.noise_std)
+        ch.update_snr(snr + 1.0)
+        out["awgn_%g_sigma_upd" % snr] = np.array(ch.noise_std)
+        out["awgn_%g_llr_upd" % snr] = ch.symbols_to_llr(ch.modulate_bpsk(bits) * 0.7)
+    for p in (0.0, 0.05, 0.3):
+        out["bsc_%g" % p] = channel.BSCChannel(p, seed=12).transmit(bits)
+    for snr in (0.0, 3.0):
+        fc = channel.RayleighFadingChannel(snr, seed=13)
+        out["ray_%g_llr" % snr] = fc.transmit(bits, return_llr=True)
+        out["ray_%g_sym" % snr] = fc.transmit(bits, return_llr=False)
+    # metrics
+    a, b = rng.randint(0, 2, 500), rng.randint(0, 2, 500)
+    out["met_a"], out["met_b"] = a, b
+    out["met_ber"] = np.array(UM.calculate_ber(a, b))
+    out["met_fer"] = np.array(UM.calculate_fer(list(a.reshape(50, 10)), list(b.reshape(50, 10))))
+    out["met_thr"] = np.array([UM.calculate_throughput(12345, t) for t in (0.0, -1.0, 0.37, 2.0)])
+    out["met_wilson"] = np.array([UM.calculate_ber_with_confidence(e, t, c) for e, t, c in
+                                  ((0, 1000, 0.95), (17, 1000, 0.95), (999, 1000, 0.9), (5, 0, 0.95),
+                                   (400, 100000, 0.99))])
+    out["met_snr"] = np.array([UM.calculate_snr_from_ebn0(e, r) for e in (-1.0, 2.0) for r in (0.25, 0.5, 0.9)])
+    out["met_ebn0"] = np.array([UM.calculate_ebn0_from_snr(e, r) for e in (-1.0, 2.0) for r in (0.25, 0.5, 0.9)])
+    return "host_api.npz", out
+
+
 JOBS = [job_scl4096_l8, job_scl1024_l8, job_ms8192, job_scl1024_l32, job_bp504,
         job_sc1024, job_ms504, job_small, job_p1, job_kat16, job_crc, job_ldpc_special, job_polar_erasures
-        ] + ROUND2_JOBS + [job_polar_nan, job_scl_l2048]
+        ] + ROUND2_JOBS + [job_polar_nan, job_scl_l2048, job_polar_single_inf, job_host_api]
 
 
 def _run(fn):

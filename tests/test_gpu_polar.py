@@ -991,3 +991,114 @@ def test_cascl_nan_frames_vs_oracle(gpu, oracle, N, L, crc):
     plan.decode(torch.from_numpy(llr).cuda(), out)
     want = oracle.cascl_decode(N, L, fr, llr, crc, threads=8)
     assert _mismatch(out.cpu().numpy(), want) == 0
+
+
+# ---------------------------------------------------------------------------
+# Round 6: a frame with exactly ONE +-inf / huge input stays
+# on the tree kernel's fast path (polar_tree.hip: no g can meet two infinities,
+# so no NaN metric), where paths can reach -inf metrics and tie there.  Pinned
+# against the reference itself (make_golden.job_polar_single_inf) and the oracle.
+
+def _single_extreme(N, fr, llr, rng):
+    """One +-inf / +-1e300 / +-1.5e308 input per frame, some frames with
+    erasures (the same kinds as make_golden.single_extreme_frames)."""
+    kinds = [(np.inf, +1, 0.0), (np.inf, -1, 0.0), (1e300, -1, 0.0), (1.5e308, +1, 0.0),
+             (np.inf, +1, 0.2), (np.inf, -1, 0.4), (1e300, +1, 0.3), (1.5e308, -1, 0.25)]
+    info = np.setdiff1d(np.arange(N), fr)
+    out = llr.copy()
+    for f in range(len(out)):
+        val, rel, er = kinds[f % len(kinds)]
+        x = out[f]
+        if er:
+            x[rng.rand(N) < er] = 0.0
+        p = int(rng.choice(fr if (f // len(kinds)) % 2 == 0 else info))
+        x[p] = (1.0 if x[p] >= 0 else -1.0) * rel * val
+    return out
+
+
+def _diag_decode_flagged(N, K, fr, L, llr, crc=None):
+    """Decode through the diagnostic library's pl_debug_polar_flagged: (bits,
+    per-frame flagged-for-redo bytes, kernel id).  The decode is the product
+    kernel; the hook only reads the NaN masks back before the redo pass."""
+    from polarcode_and_ldpc_amd import _native
+    D = _native.load_diag()
+    if D is None:
+        pytest.skip("diagnostic library not built (make -C polarcode_and_ldpc_amd/csrc diag)")
+    mask = np.zeros(N, np.uint8)
+    mask[fr] = 1
+    h = ctypes.c_void_p()
+    assert D.pl_polar_plan_create(N, K, mask.ctypes.data_as(ctypes.c_void_p), L, 0, ctypes.byref(h)) == 0
+    try:
+        info = _native.PlanInfo()
+        assert D.pl_plan_get_info(h, ctypes.byref(info)) == 0
+        if crc is not None:
+            assert D.pl_polar_plan_set_crc(h, crc[0], crc[1]) == 0
+        x = torch.from_numpy(np.ascontiguousarray(llr)).cuda()
+        out = torch.empty((len(llr), K), dtype=torch.uint8, device="cuda")
+        flagged = np.full(len(llr), 7, np.uint8)
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        rc = D.pl_debug_polar_flagged(h, ctypes.c_void_p(x.data_ptr()), len(llr), N, ctypes.c_void_p(out.data_ptr()),
+                                      flagged.ctypes.data_as(ctypes.c_void_p), st)
+        assert rc == 0, D.pl_last_error()
+        torch.cuda.synchronize()
+        return out.cpu().numpy().astype(np.int64), flagged, int(info.reserved)
+    finally:
+        D.pl_plan_destroy(h)
+
+
+def test_single_extreme_input_golden_fast_path(gpu):
+    """Reference decodes of one-+-inf / one-huge-input frames (N=1024 L=8 / L=32,
+    N=2048 / 4096 L=8): bit-exact, on the tree kernel, and NOT flagged for the
+    redo decoder -- while a NaN frame and a two-inf frame in the same batch are
+    (the hook's positive control)."""
+    d = golden("polar_single_inf.npz")
+    for N in (1024, 2048, 4096):
+        fr, llr = d["N%d_frozen" % N], d["N%d_llr" % N]
+        K = N - len(fr)
+        ctrl = llr[:2].copy()
+        ctrl[0, 3] = np.nan
+        ctrl[1, [5, 9]] = [np.inf, -np.inf]
+        for L in d["N%d_Ls" % N]:
+            L = int(L)
+            want = d["N%d_L%d" % (N, L)]
+            dec = _P().SCLDecoder(N, K, list_size=L, frozen_bits=fr)
+            assert dec.plan.info.reserved == 4, (N, L)  # the tree kernel
+            assert _mismatch(dec.decode_batch(llr), want) == 0, (N, L)
+            bits, flagged, kern = _diag_decode_flagged(N, K, fr, L, np.concatenate([llr, ctrl]))
+            assert kern == 4
+            assert _mismatch(bits[:len(llr)], want) == 0, (N, L)
+            assert not flagged[:len(llr)].any(), (N, L, np.nonzero(flagged)[0])
+            assert flagged[len(llr):].all(), (N, L)
+
+
+@pytest.mark.parametrize("N,L,B", [(1024, 8, 65536), (1024, 32, 65536), (2048, 8, 32768), (4096, 8, 16384)])
+def test_single_extreme_frames_in_large_batch(gpu, oracle, N, L, B):
+    """Single-extreme-input frames scattered over a BASELINE-size batch of noisy
+    frames (1 dB): plain SCL and CA-SCL (CRC-8) against the oracle, and none of
+    them flagged."""
+    from polarcode_and_ldpc_amd.polar.utils import CRC_POLYNOMIALS
+    P = _P()
+    K = N // 2
+    fr = P.construct_frozen_set(N, K, 2.0)
+    rng = np.random.RandomState(N + 3 * L)
+    msg = rng.randint(0, 2, (B, K))
+    cw = P.PolarEncoder(N, K, frozen_bits=fr).encode_batch(msg)
+    sigma = np.sqrt(1.0 / (2.0 * 10 ** 0.1))
+    llr = 2.0 * ((1.0 - 2.0 * cw) + sigma * rng.randn(B, N)) / sigma ** 2
+    rows = np.unique(np.concatenate([rng.choice(B, 46, replace=False), [0, 1, B - 1]]))
+    llr[rows] = _single_extreme(N, fr, llr[rows], rng)
+    chk = np.unique(np.concatenate([rows, rng.choice(B, 24, replace=False)]))
+    for crc in (None, "CRC-8"):
+        c = None if crc is None else (8, CRC_POLYNOMIALS[crc])
+        bits, flagged, kern = _diag_decode_flagged(N, K, fr, L, llr, crc=c)
+        assert kern == 4 and not flagged.any(), np.nonzero(flagged)[0][:8]
+        if crc is None:
+            want = oracle.scl_decode(N, L, fr, llr[chk], threads=8)
+        else:
+            want = oracle.cascl_decode(N, L, fr, llr[chk], crc, threads=8)
+        assert _mismatch(bits[chk], want) == 0, crc
+        # the product library gives the same bits for the whole batch
+        dec = P.SCLDecoder(N, K, list_size=L, frozen_bits=fr)
+        if crc is not None:
+            dec.plan.set_crc(*c)
+        assert _mismatch(dec.decode_batch(llr), bits) == 0, crc

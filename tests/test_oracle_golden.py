@@ -232,3 +232,16 @@ def test_scl_above_1024(oracle):
     d = golden("polar_scl_l2048.npz")
     for tag, N, L in (("N64_L2048", 64, 2048), ("N32_L1500", 32, 1500)):
         assert _bad(oracle.scl_decode(N, L, d[tag + "_frozen"], d[tag + "_llr"], threads=8), d[tag + "_scl"]) == 0, tag
+
+
+def test_scl_single_extreme_input(oracle):
+    """Frames with exactly one +-inf / +-1e300 / +-1.5e308 channel LLR (some with
+    erasures), decoded by the reference (make_golden.job_polar_single_inf,
+    round 6): paths reach -inf metrics and tie there; the stable sort keeps
+    their candidate order (decoder.py:306-307)."""
+    d = golden("polar_single_inf.npz")
+    for N in (1024, 2048, 4096):
+        fr, llr = d["N%d_frozen" % N], d["N%d_llr" % N]
+        assert (~np.isfinite(llr) | (np.abs(llr) >= 2.0 ** 1000)).sum(axis=1).max() <= 1
+        for L in d["N%d_Ls" % N]:
+            assert _bad(oracle.scl_decode(N, int(L), fr, llr, threads=8), d["N%d_L%d" % (N, L)]) == 0, (N, L)

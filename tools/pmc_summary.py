@@ -36,6 +36,7 @@ KEYS = {
     "polar_sc_1024_default": ("g2", "pl::polar_tree_kernel<10, 1, true, 1, 5, false, 2, 0>", 65536),
     "polar_sc_256": ("g2", "pl::polar_tree_kernel<8, 1, true, 1, 3, false, 2, 0>", 100),
     "ldpc_ms_8192": ("g2", "pl::ldpc_ms_compact_kernel", 131072),
+    "ldpc_bp_504_valid": ("g2", "pl::ldpc_bp_grp_kernel<3, 6, 2, false>", 65536),
 }
 PASSES = ("fetch", "write", "valu", "mix", "l2", "wait")
 F64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
@@ -107,13 +108,15 @@ def main(src, dst):
             shutil.copy(os.path.join(gs, "bench_trace.json"), os.path.join(dst, "bench_trace_%s.json" % g))
         allsumm[g] = summarise(gs)
     json.dump(allsumm, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1, sort_keys=True)
+    bid = os.path.join(src, "build_id.txt")  # the profiled libpolarldpc.so (tools/gpu_profile.sh)
+    build = open(bid).read().strip() if os.path.exists(bid) else None
     tp = os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_traffic.json")
     traffic = json.load(open(tp)) if os.path.exists(tp) else {}
     for key, (g, prefix, frames) in KEYS.items():
         for name, s in allsumm.get(g, {}).items():
             if name.startswith(prefix) and "hbm_bytes_per_launch" in s:
                 t = dict(bytes_per_launch=s["hbm_bytes_per_launch"], frames=frames, kernel=name,
-                         source=os.path.join(dst, "pmc_summary.json") + " [%s]" % g)
+                         source=os.path.join(dst, "pmc_summary.json") + " [%s]" % g, build=build)
                 if "SQ_INSTS_VALU" in s:
                     t["valu_per_launch"] = s["SQ_INSTS_VALU"]
                 if "valu_fp64_per_launch" in s:

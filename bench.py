@@ -555,7 +555,8 @@ def bench_config0(args, rt, pool):
 
 # ---------------------------------------------------------------- LDPC
 LDPC_KERNELS = {1: "ldpc_decode_kernel<BP>", 2: "ldpc_reg_kernel<BP,DV=3>", 3: "ldpc_check_kernel<BP>",
-                5: "ldpc_ms_compact_kernel<8,3,6,true>", 7: "ldpc_bp_grp_kernel<3,6,2,false>"}
+                5: "ldpc_ms_compact_kernel<8,3,6,true>", 7: "ldpc_bp_grp_kernel<3,6,2,false>",
+                8: "ldpc_ms36_kernel<8>"}
 
 
 def ldpc_kernel_name(plan):

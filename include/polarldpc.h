@@ -155,11 +155,13 @@ const char* pl_last_error(void);
 
 /* Diagnostic build only (make DIAG=1; the product library returns
  * PL_EUNSUPPORTED): pl_decode of a polar plan through an instrumented kernel that adds
- * per-phase s_memtime cycle totals (summed over all frames) into stamps_dev[8]:
+ * per-phase s_memtime cycle totals (summed over all frames) into stamps_dev[16]:
  * tree kernel (pl_plan_info.reserved == 4): [0] fused top, [1] workspace chains,
  * [2] LDS chain, [3] path metrics, [4] pruning/cloning, [5] partial-sum walk,
- * [6] final selection/output, [7] workspace fences.  Timing differs from
- * pl_decode; read shares. */
+ * [6] final selection/output, [7] workspace fences; then counts of the
+ * path-metric evaluations: [8] per-wave calls, [9] calls with a lane that
+ * evaluates log1p(e^-x), [10] such lanes, [11] active lanes.  Timing differs
+ * from pl_decode; read shares. */
 int pl_debug_polar_stamps(pl_plan* plan, const double* llr_dev, int64_t batch, int64_t ld, uint8_t* bits_dev,
                           unsigned long long* stamps_dev, void* stream);
 

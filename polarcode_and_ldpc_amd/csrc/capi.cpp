@@ -127,7 +127,8 @@ static int check_device(const pl_plan* p) {
 // the metric evaluation of the list kernel a plan's NaN frames come from (polar_nan.hip)
 static int redo_metric(const pl_plan* p) {
     if (!p->tree && !p->generic) return pl::kRedoMetricLane;
-    return p->pg.N <= (1 << PL_METRIC_FUSED_NMAX) ? pl::kRedoMetricFused : pl::kRedoMetricLean;
+    if (p->pg.N > (1 << PL_METRIC_FUSED_NMAX)) return pl::kRedoMetricLean;
+    return PL_METRIC_TAB ? pl::kRedoMetricTab : pl::kRedoMetricFused;
 }
 
 // ldpc_bp_grp_kernel's variable -> thread-slot map (slot q = 256 j + tid;
@@ -513,6 +514,29 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
             g.lds_bytes = (int)((lds_c + 15) & ~(size_t)15);
         }
     }
+    // (3,6)-regular min-sum of n = 2048 / 4096 / 8192 (the BASELINE n = 8192 code):
+    // ldpc_ms36_kernel (PL_LDPC_KERNEL=compact keeps ldpc_ms_compact_kernel)
+    g.ms36 = 0;
+    std::vector<int32_t> ms_vw;
+    if (g.compact && g.regular && maxdv == 3 && maxdc == 6 && 2 * m == n && pl::ldpc_ms36_lds(n) > 0 &&
+        !(lk && std::string(lk) == "compact")) {
+        g.ms36 = n / 1024;
+        g.lds_bytes = pl::ldpc_ms36_lds(n);
+        const uint32_t REC = 8u * (uint32_t)n, MET = 16u * (uint32_t)n;  // ldpc_ms36_kernel's LDS layout
+        // [n][8]: per variable its three edge words and meta addresses; then
+        // [m][4]: per check the LDS byte addresses 8v of its six variables, two per word
+        ms_vw.assign((size_t)n * 8 + (size_t)m * 4, 0);
+        for (int v = 0; v < n; ++v)
+            for (int k = 0; k < 3; ++k) {
+                const int e = var_edge[var_ptr[v] + k], c = edge_chk[e], pos = e - row_ptr[c];
+                ms_vw[(size_t)v * 8 + k] = (int32_t)((REC + 16u * (uint32_t)c) | (3u * (uint32_t)pos));
+                ms_vw[(size_t)v * 8 + 3 + k] = (int32_t)(MET + 4u * (uint32_t)c);
+            }
+        for (int c = 0; c < m; ++c)
+            for (int k = 0; k < 3; ++k)
+                ms_vw[(size_t)n * 8 + (size_t)c * 4 + k] =
+                    (int32_t)((8u * (uint32_t)col_idx[row_ptr[c] + 2 * k]) | ((8u * (uint32_t)col_idx[row_ptr[c] + 2 * k + 1]) << 16));
+    }
     if (g.check_kernel) {
         g.threads = 256;
         g.lds_bytes = (int)(((size_t)(2 * (size_t)E + n) * 8 + 15) & ~(size_t)15);
@@ -538,6 +562,9 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     const size_t grp_at = all.size();
     all.insert(all.end(), grp_meta.begin(), grp_meta.end());
     all.insert(all.end(), var_tpos.begin(), var_tpos.end());
+    all.resize((all.size() + 3) & ~(size_t)3, 0);  // ms_vw: 16-byte aligned (uint4 loads)
+    const size_t vw_at = all.size();
+    all.insert(all.end(), ms_vw.begin(), ms_vw.end());
     hipError_t e = upload(&p->d_ldpc, all);
     if (e != hipSuccess) { pl_plan_destroy(p); return hipfail(e, "plan upload"); }
     p->ld.row_ptr = p->d_ldpc;
@@ -550,6 +577,7 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
     p->ld.var_cp = p->ld.var_chk + E;
     p->ld.grp_meta = g.grp ? p->d_ldpc + grp_at : nullptr;
     p->ld.var_tpos = g.grp ? p->d_ldpc + grp_at + grp_meta.size() : nullptr;
+    p->ld.ms_vw = g.ms36 ? reinterpret_cast<const uint32_t*>(p->d_ldpc + vw_at) : nullptr;
     if ((e = pl::ldpc_prepare(g)) != hipSuccess) { pl_plan_destroy(p); return hipfail(e, "hipFuncSetAttribute"); }
     p->ws_unit = pl::ldpc_work_bytes_per_frame(g);
     p->ldpc_chunk = std::max(1, env_int("PL_LDPC_CHUNK", 16384));
@@ -984,8 +1012,9 @@ extern "C" int pl_plan_get_info(const pl_plan* p, pl_plan_info* info) {
         info->kind = 1; info->n_in = p->lg.n; info->n_out = p->lg.n; info->list_size = 0;
         info->lds_bytes = p->lg.lds_bytes; info->fused_top = 0; info->frames_per_block = 1;
         // kernel: 2 register-cached, 7 register-cached BP with degree-grouped products,
-        // 1 generic (LDS or global workspace), 3 thread-per-check, 5 min-sum with compressed check state
-        info->reserved = p->lg.compact ? 5 : (p->lg.check_kernel ? 3 : (p->lg.grp ? 7 : (p->lg.reg_variant ? 2 : 1)));
+        // 1 generic (LDS or global workspace), 3 thread-per-check, 5 min-sum with compressed check state,
+        // 8 (3,6)-regular min-sum with rebuild-ready check state
+        info->reserved = p->lg.ms36 ? 8 : p->lg.compact ? 5 : (p->lg.check_kernel ? 3 : (p->lg.grp ? 7 : (p->lg.reg_variant ? 2 : 1)));
     }
     return PL_OK;
 }

@@ -10,6 +10,11 @@
 // de-duplicated fused top -- every tree instance (n <= 12) now uses it
 #define PL_METRIC_FUSED_NMAX 12
 #endif
+#ifndef PL_METRIC_TAB
+// 1: the tree instances evaluate log1p(exp(-x)) from a 770-row table
+// (log1p_exp_neg_tab, fp64_math.hpp) instead of the fused exp + log1p
+#define PL_METRIC_TAB 0
+#endif
 
 namespace pl {
 
@@ -83,8 +88,9 @@ int nan_redo_lds_bytes(int list_size);
 hipError_t nan_redo_prepare(int list_size);
 // path-metric evaluation of the list kernel whose frames are redone: the lane
 // kernel's path_metrics (libm-style log1p(exp(-x))), or the tree instances'
-// path_metrics_fast with the fused (n <= PL_METRIC_FUSED_NMAX) or lean form
-enum RedoMetric { kRedoMetricLane = 0, kRedoMetricFused = 1, kRedoMetricLean = 2 };
+// path_metrics_fast with the fused (n <= PL_METRIC_FUSED_NMAX) or lean form, or
+// the table form (PL_METRIC_TAB)
+enum RedoMetric { kRedoMetricLane = 0, kRedoMetricFused = 1, kRedoMetricLean = 2, kRedoMetricTab = 3 };
 hipError_t nan_redo_launch(const double* llr, int64_t ld, uint8_t* out, int64_t batch, int N, int K, int Lsz,
                            const uint32_t* frozen_dec, const int32_t* info_pos, const uint32_t* crc_g,
                            uint64_t* masks, int grid, int fpw, int metric, unsigned char* scratch,
@@ -128,6 +134,7 @@ struct LdpcGeom {
     int grp;           // BP reg variant: ldpc_bp_grp_kernel (degree-grouped products, padded T'/C')
     int tl;            // grp: length of the padded T'/C' arrays (doubles)
     int npad;          // grp: pad positions listed after the variable slots (a multiple of 256, -1 filled)
+    int ms36;          // > 0: ldpc_ms36_kernel<ms36> ((3,6)-regular min-sum, n = 1024 ms36)
 };
 struct LdpcDev {
     const int32_t* row_ptr;   // [m+1]
@@ -144,6 +151,11 @@ struct LdpcDev {
     // checks, then [q] the variable (-1: none); then npad pad positions
     const int32_t* grp_meta;  // [256 EPT]
     const int32_t* var_tpos;  // [256 VPT (2 DV + 1)]
+    // ms36 (ldpc_ms36_kernel), 16-byte aligned: per variable [8] u32, its three
+    // edge words (LDS rec address of the check | 3 * position) then the three
+    // LDS meta addresses, in the reference's np.sum order (ascending check);
+    // then per check [4] u32, the LDS addresses 8v of its six variables, two per word
+    const uint32_t* ms_vw;    // [n][8] + [m][4]
 };
 hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, int64_t ld,
                        uint8_t* bits, int32_t* iters, int64_t batch, double* work, hipStream_t s);
@@ -157,5 +169,6 @@ int ldpc_reg_variant(int dv, int E, int n);  // 0: none fits
 size_t ldpc_reg_list_bytes(int variant);      // BP tanh lists of an ldpc_reg_kernel instance
 int ldpc_reg_ept(int variant);                // edges per thread of an ldpc_reg_kernel instance
 int ldpc_reg_vpt(int variant);                // variables per thread
+int ldpc_ms36_lds(int n);                     // LDS of the ldpc_ms36_kernel instance for n (0: none)
 
 }  // namespace pl

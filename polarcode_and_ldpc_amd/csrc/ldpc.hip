@@ -22,6 +22,8 @@
 //   ldpc_decode_kernel<ALGO, GLOBAL, ..> any code, LDS or global-workspace state;
 //   ldpc_ms_compact_kernel               min-sum for codes whose T/C exceed LDS:
 //                                        compressed per-check statistics in LDS;
+//   ldpc_ms36_kernel<VPT>                the same for (3,6)-regular n = 1024 VPT
+//                                        (the BASELINE n = 8192 code);
 //   ldpc_check_kernel<ALGO>              thread-per-check variant (diagnostic).
 #include "common.hpp"
 #include "internal.hpp"
@@ -29,6 +31,7 @@
 
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 namespace pl {
 
@@ -1127,6 +1130,276 @@ ldpc_ms_compact_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, i
     if (iters && tid == 0) iters[frame] = done;
 }
 
+// ---- min-sum on (3,6)-regular codes of n = 1024 VPT (ldpc_ms36_kernel) ------
+// The BASELINE n = 8192 code (configs[4]): the passes, state size and
+// arithmetic of ldpc_ms_compact_kernel, with the check state stored in the form
+// both passes rebuild a check-to-variable message from in a few instructions
+// (the compact kernel spent ~46 VALU lane-operations per edge-iteration, 94 %
+// of them integer / select / move: VERDICT r05).
+//   rec[c] = (A, B), meta[c] (u32): output k of check c is (k == idx1 ? B : A)
+//   with its sign bit XORed with flip_k.  meta bits: flip_k at bit (3k + 31) mod
+//   32, sel_k = (k == idx1) at bit 3k + 3, 3 idx1 at bits 20-23.
+// Every min-sum check fits this form.  No zero and no NaN input: A, B = min1 *
+// norm, min2 * norm, idx1 the first position of min1, flip_k = parity of the
+// negative inputs XOR input k's sign (sp * mn * norm with sp = +-1 is exactly
+// +-(mn * norm)).  Otherwise (ms_c2v's rules, decoder.py:257-287): two or more
+// NaN inputs -> every output NaN; one -> every output but the NaN position's
+// NaN; no NaN, two or more zeros -> every output +-0; one zero -> every output
+// but the zero's +-0: at most one position differs from the rest, so the
+// outputs, computed exactly by ms_c2v, are encoded as |A| | |B| | signs.  The
+// rebuilt messages are therefore bit-identical to ms_c2v's.
+// Odd checks store meta rotated by 16 bits: a variable's edge word (the check's
+// rec address | 3 pos; bit 4 of it is the check's parity) is then the rotation
+// that brings flip_pos to bit 31 and sel_pos to bit 3 (v_alignbit), and the rec
+// address of its magnitude is (word & ~15) | (rotated & 8).
+// LDS: tot[n] at 0 (16-bit byte addresses 8v, two per register), rec[m] at 8n,
+// meta[m] at 16n, vote words at 18n (n = 8192: 144.1 KB, as the compact kernel).
+struct Ms36State {
+    double2 st;
+    uint32_t meta0;
+};
+
+// ldpc_ms36_kernel's check state for a check with a zero or NaN input (rare:
+// out of line, so its registers do not weigh on the kernel's common path): the
+// exact outputs (ms_c2v), encoded as (A, B, idx1, signs).
+#ifndef PL_MS36_NOINLINE
+#define PL_MS36_NOINLINE 0
+#endif
+#if PL_MS36_NOINLINE
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+Ms36State ms36_special(double x0, double x1, double x2, double x3, double x4, double x5,
+                                               double norm) {
+    constexpr int DC = 6;
+    const double x[DC] = {x0, x1, x2, x3, x4, x5};
+    double2 mm;
+    uint32_t gm;
+    ms_state<DC>(x, mm, gm);
+    uint64_t u[DC];
+    uint32_t f = 0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const uint64_t b = (uint64_t)__double_as_longlong(ms_c2v(mm, gm, k, norm));
+        u[k] = b & 0x7FFFFFFFFFFFFFFFull;
+        f |= (uint32_t)(b >> 63) << ((3 * k + 31) & 31);
+    }
+    uint32_t id = 0;
+    uint64_t A, B;
+    if (u[0] == u[1]) {  // position 0 is not the odd one: the first differing position is
+        A = u[0];
+#pragma unroll
+        for (int k = DC - 1; k >= 2; --k) id = u[k] != A ? (uint32_t)k : id;
+        B = u[id];
+    } else if (u[2] == u[0]) {
+        A = u[0]; id = 1; B = u[1];
+    } else {
+        A = u[1]; id = 0; B = u[0];
+    }
+    Ms36State r;
+    r.st = make_double2(__longlong_as_double((long long)A), __longlong_as_double((long long)B));
+    r.meta0 = f | (8u << (3 * id)) | ((3 * id) << 20);
+    return r;
+}
+
+#ifndef PL_MS36_CB
+#define PL_MS36_CB 2  // checks whose loads issue together
+#endif
+#ifndef PL_MS36_CREG
+#define PL_MS36_CREG 0  // 1: check adjacency in registers (spills), 0: one 16-byte load per check
+#endif
+template <int VPT>
+__global__ void __launch_bounds__(1024)
+ldpc_ms36_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
+                 uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch) {
+    constexpr int N = 1024 * VPT, M = N / 2, MQ = VPT / 2, DC = 6;
+    constexpr uint32_t REC = 8u * N, MET = REC + 16u * M, VOTE = MET + 4u * M;
+    constexpr uint32_t FMASK = 0x80004924u;  // flip bits of positions 0..5: 31, 2, 5, 8, 11, 14
+    static_assert(8 * (N - 1) < 65536 && REC % 32 == 0 && MQ >= 1, "ldpc_ms36_kernel geometry");
+    // static LDS: its base address is the constant 0, so the byte addresses need no base added
+    __shared__ __attribute__((aligned(16))) unsigned char smem[VOTE + 128];
+    const int64_t frame = blockIdx.x;
+    if (frame >= batch) return;
+    const int tid = threadIdx.x;
+    double* tot = reinterpret_cast<double*>(smem);
+    double2* rec = reinterpret_cast<double2*>(smem + REC);
+    uint32_t* met = reinterpret_cast<uint32_t*>(smem + MET);
+    uint32_t* vote = reinterpret_cast<uint32_t*>(smem + VOTE);
+    const double* __restrict__ ch = llr + frame * ld;
+    const int32_t* __restrict__ ci = dv.col_idx;
+    const uint4* __restrict__ vw = reinterpret_cast<const uint4*>(dv.ms_vw);
+    const double norm = g.norm;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) tot[tid + 1024 * j] = ch[tid + 1024 * j];
+    // the tot byte addresses of the DC variables of checks tid + 1024 q, two per
+    // word: in registers (PL_MS36_CREG) or read per check from the plan (ms_cw)
+    uint32_t ccol[PL_MS36_CREG ? MQ : 1][DC / 2];
+    if constexpr (PL_MS36_CREG) {
+#pragma unroll
+        for (int q = 0; q < MQ; ++q) {
+            const int c = tid + 1024 * q;
+#pragma unroll
+            for (int k = 0; k < DC / 2; ++k)
+                ccol[q][k] = (8u * (uint32_t)ci[c * DC + 2 * k]) | ((8u * (uint32_t)ci[c * DC + 2 * k + 1]) << 16);
+        }
+    }
+    const uint4* __restrict__ cw = reinterpret_cast<const uint4*>(dv.ms_vw + 8 * N);
+    const uint32_t rot = 16u * (uint32_t)(tid & 1);  // this thread's checks' parity (c = tid + 1024 q)
+    __syncthreads();
+
+    // one check: its DC inputs (x = tv - c2v, or tv at iteration 0) -> new state
+    auto check_state = [&](const double* x, double2& st, uint32_t& meta0) {
+        bool ord = true;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) ord &= fabs(x[k]) > 0.0;  // false for +-0 and NaN
+        if (ord) {
+            // no NaN and no zero: (min1, min2) = (min(min1, a), min(min2, max(min1, a)))
+            // is the reference scan's (lt ? a : min1, lt ? min1 : min(min2, a)), as
+            // three v_min/v_max_f64 (inline: no NaN can reach them, so minnum's
+            // quieting canonicalisations are not needed)
+            double min1 = fabs(x[0]), min2 = __builtin_inf();
+            uint32_t i3 = 0, ng = (uint32_t)__double2hiint(x[0]) & 0x80000000u;
+#pragma unroll
+            for (int k = 1; k < DC; ++k) {
+                const bool lt = fabs(x[k]) < min1;
+                double mx;
+                asm("v_max_f64 %0, %1, |%2|" : "=v"(mx) : "v"(min1), "v"(x[k]));
+                asm("v_min_f64 %0, %1, %2" : "=v"(min2) : "v"(min2), "v"(mx));
+                asm("v_min_f64 %0, %1, |%2|" : "=v"(min1) : "v"(min1), "v"(x[k]));
+                i3 = lt ? 3u * k : i3;
+                ng |= ((uint32_t)__double2hiint(x[k]) >> 31) << (3 * k - 1);
+            }
+            const uint32_t flips = ng ^ ((__popc(ng) & 1) ? FMASK : 0u);
+            meta0 = flips | (8u << i3) | (i3 << 20);
+            st = make_double2(min1 * norm, min2 * norm);
+        } else {
+            const Ms36State r = ms36_special(x[0], x[1], x[2], x[3], x[4], x[5], norm);
+            st = r.st;
+            meta0 = r.meta0;
+        }
+    };
+
+    // check pass: checks tid + 1024 q; the loads of two checks issue before either is reduced
+    auto check_pass = [&](auto first_tag) -> int {
+        constexpr bool FIRST = decltype(first_tag)::value;
+        int syn = 0;
+        int ct = tid;  // opaque: the check words are re-read every iteration (see the variable pass)
+        asm volatile("" : "+v"(ct));
+        constexpr int CB = MQ >= PL_MS36_CB ? PL_MS36_CB : 1;
+#pragma unroll
+        for (int q0 = 0; q0 < MQ; q0 += CB) {
+            double tv[CB][DC];
+            double2 om[CB];
+            uint32_t omt[CB];
+#pragma unroll
+            for (int b = 0; b < CB; ++b) {
+                const int c = tid + 1024 * (q0 + b);
+                uint32_t cc[DC / 2];
+                if constexpr (PL_MS36_CREG) {
+#pragma unroll
+                    for (int k = 0; k < DC / 2; ++k) cc[k] = ccol[q0 + b][k];
+                } else {
+                    const uint4 w4 = cw[ct + 1024 * (q0 + b)];
+                    cc[0] = w4.x; cc[1] = w4.y; cc[2] = w4.z;
+                }
+#pragma unroll
+                for (int k = 0; k < DC; ++k) {
+                    const uint32_t a = (cc[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                    tv[b][k] = *reinterpret_cast<const double*>(smem + a);
+                }
+                if (!FIRST) {
+                    om[b] = rec[c];
+                    omt[b] = met[c];
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < CB; ++b) {
+                if constexpr (PL_MS_PRIO >= 2) ms_prio(q0 + b, MQ);
+                const int c = tid + 1024 * (q0 + b);
+                double x[DC];
+                if constexpr (FIRST) {
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) x[k] = tv[b][k];
+                } else {
+                    const uint32_t m0 = __builtin_amdgcn_alignbit(omt[b], omt[b], rot);
+                    const uint32_t i3 = (m0 >> 20) & 15u;
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) {
+                        const double mag = i3 == 3u * k ? om[b].y : om[b].x;
+                        const uint32_t s = k == 0 ? m0 : m0 << (32 - 3 * k);
+                        const double c2v = __hiloint2double(__double2hiint(mag) ^ (int)(s & 0x80000000u),
+                                                            __double2loint(mag));
+                        x[k] = tv[b][k] - c2v;
+                    }
+                }
+                int sp = 0;
+#pragma unroll
+                for (int k = 0; k < DC; ++k) sp ^= (tv[b][k] <= 0.0) ? 1 : 0;
+                syn |= sp;
+                double2 st;
+                uint32_t meta0;
+                check_state(x, st, meta0);
+                rec[c] = st;
+                met[c] = __builtin_amdgcn_alignbit(meta0, meta0, rot);
+            }
+        }
+        return syn;
+    };
+
+    int done = g.max_iter;
+    for (int it = 0; it < g.max_iter; ++it) {
+        // opaque each iteration: the packed addresses stay packed (see ldpc_ms_compact_kernel)
+        if constexpr (PL_MS36_CREG) {
+#pragma unroll
+            for (int q = 0; q < MQ; ++q)
+#pragma unroll
+                for (int k = 0; k < DC / 2; ++k) asm volatile("" : "+v"(ccol[q][k]));
+        }
+        const int syn = it == 0 ? check_pass(std::integral_constant<bool, true>())
+                                : check_pass(std::integral_constant<bool, false>());
+        // the variable pass reads the channel row and its edge words again every
+        // iteration (L2): an opaque index keeps the compiler from holding them in
+        // registers across iterations (spilled: 40 VGPRs)
+        int vt = tid;
+        asm volatile("" : "+v"(vt));
+        if (g.early_stop && it > 0) {
+            if (!wg_any(syn != 0, vote, it & 1)) { done = it; break; }
+        } else {
+            __syncthreads();
+        }
+        // variable pass: total = llr + np.sum of the 3 rebuilt messages (sequential)
+#pragma unroll
+        for (int j = 0; j < VPT; ++j) {
+            if constexpr (PL_MS_PRIO) ms_prio(j, VPT);
+            const int v = tid + 1024 * j;
+            const int vo = vt + 1024 * j;
+            const uint4 wa = vw[2 * vo], wb = vw[2 * vo + 1];  // w0 w1 w2 ma0 | ma1 ma2 - -
+            const double chv = ch[vo];
+            const uint32_t w[3] = {wa.x, wa.y, wa.z}, ma[3] = {wa.w, wb.x, wb.y};
+            double sum = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint32_t mt = *reinterpret_cast<const uint32_t*>(smem + ma[k]);
+                const uint32_t t = __builtin_amdgcn_alignbit(mt, mt, w[k]);
+                const double mag = *reinterpret_cast<const double*>(smem + ((w[k] & ~15u) | (t & 8u)));
+                sum += __hiloint2double(__double2hiint(mag) ^ (int)(t & 0x80000000u), __double2loint(mag));
+            }
+            tot[v] = chv + sum;
+        }
+        __syncthreads();
+    }
+    uint8_t* o = bits + frame * (int64_t)N;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) o[tid + 1024 * j] = tot[tid + 1024 * j] <= 0.0 ? 1 : 0;
+    if (iters && tid == 0) iters[frame] = done;
+}
+
+// LDS bytes of ldpc_ms36_kernel<n / 1024> (0: no instance for this code)
+int ldpc_ms36_lds(int n) {
+    return (n == 2048 || n == 4096 || n == 8192) ? 18 * n + 128 : 0;
+}
+
 #if PL_DIAG
 // Thread-per-check kernel: one workgroup (256 threads) per frame, all state in
 // LDS: C[E] (check-to-variable), T[E] (check inputs), tot[n].  Checks are
@@ -1236,6 +1509,11 @@ static void* pick(bool global) {
 }
 
 static void* pick_kernel(const LdpcGeom& g) {
+    if (g.ms36) {
+        if (g.ms36 == 2) return (void*)ldpc_ms36_kernel<2>;
+        if (g.ms36 == 4) return (void*)ldpc_ms36_kernel<4>;
+        return (void*)ldpc_ms36_kernel<8>;
+    }
     if (g.compact) {
         if (g.n <= 8192 && g.regular && g.maxdv == 3 && g.maxdc == 6) {
             // pre-scaled check state for |normalization| <= 1 (every BASELINE min-sum decode)
@@ -1271,9 +1549,12 @@ hipError_t ldpc_launch_stamped(const LdpcGeom& g, const LdpcDev& d, const double
 }
 #endif
 
+// ldpc_ms36_kernel's LDS is static (declared in the kernel); the others' dynamic
+static int dyn_lds(const LdpcGeom& g) { return g.ms36 ? 0 : g.lds_bytes; }
+
 hipError_t ldpc_prepare(const LdpcGeom& g) {
     void* k = pick_kernel(g);
-    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds_bytes);
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, dyn_lds(g));
 }
 
 hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, int64_t ld,
@@ -1283,7 +1564,7 @@ hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, i
     LdpcDev dd = d;
     void* args[] = {&gg, &dd, (void*)&llr, (void*)&ld, (void*)&bits, (void*)&iters, (void*)&batch,
                     (void*)&work};
-    return hipLaunchKernel(k, dim3((unsigned)batch), dim3(g.threads), args, g.lds_bytes, s);
+    return hipLaunchKernel(k, dim3((unsigned)batch), dim3(g.threads), args, dyn_lds(g), s);
 }
 
 }  // namespace pl

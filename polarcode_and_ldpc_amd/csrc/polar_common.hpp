@@ -49,22 +49,39 @@ PL_DEV void path_metrics(double pm, double lam, double& m0, double& m1) {
     if (WANT1) m1 = pm + ((lam >= 0.0) ? -lam - t : -t);
 }
 
-// Same increments for the tree kernel, with a cheaper skip test (hardware
-// frexp exponents: frexp_exp = ilogb + 1 for finite nonzero values, so the
-// threshold is identical) and two more skips that cannot change a result:
-// inactive list slots (their metrics are never read) and pm = +-inf with a
-// non-NaN LLR (t is finite, so pm + anything finite = pm as in the reference).
-template <bool WANT1, bool FUSED = false>
-PL_DEV void path_metrics_fast(double pm, double lam, bool active, double& m0, double& m1) {
+// whether path_metrics_fast must evaluate log1p(e^-|lam|) for this lane (else
+// the term is below a quarter ulp of every addend, or the lane is idle)
+PL_DEV bool metric_needs_t(double pm, double lam, bool active) {
     const double x = fabs(lam);
     const int ep = __builtin_amdgcn_frexp_exp(pm);
     const int ex = __builtin_amdgcn_frexp_exp(x);
     const int e = ep < ex ? ep : ex;
     const bool finite_pm = __builtin_isfinite(pm);
-    const bool skip = !active || (!finite_pm && !__builtin_isnan(x)) ||
-                      (finite_pm && pm != 0.0 && x > (double)(57 - e) * 0.6931471805599453);
+    return !(!active || (!finite_pm && !__builtin_isnan(x)) ||
+             (finite_pm && pm != 0.0 && x > (double)(57 - e) * 0.6931471805599453));
+}
+
+
+// Same increments for the tree kernel, with a cheaper skip test (hardware
+// frexp exponents: frexp_exp = ilogb + 1 for finite nonzero values, so the
+// threshold is identical) and two more skips that cannot change a result:
+// inactive list slots (their metrics are never read) and pm = +-inf with a
+// non-NaN LLR (t is finite, so pm + anything finite = pm as in the reference).
+// t = log1p(exp(-x)), x >= 0, in the list kernels' evaluations (fp64_math.hpp):
+// FORM 0 lean exp + log1p, 1 fused, 2 table
+template <int FORM>
+PL_DEV double metric_t(double x) {
+    if constexpr (FORM == 2) return log1p_exp_neg_tab(x);
+    else if constexpr (FORM == 1) return log1p_exp_neg(x);
+    else return log1p_pos(exp_neg(x));
+}
+
+template <bool WANT1, int FORM = 0>
+PL_DEV void path_metrics_fast(double pm, double lam, bool active, double& m0, double& m1) {
+    const double x = fabs(lam);
+    const bool skip = !metric_needs_t(pm, lam, active);
     double t = 0.0;
-    if (!skip) t = FUSED ? log1p_exp_neg(x) : log1p_pos(exp_neg(x));  // lean exp / log1p (fp64_math.hpp)
+    if (!skip) t = metric_t<FORM>(x);
     m0 = pm + ((lam >= 0.0) ? -t : lam - t);
     if (WANT1) m1 = pm + ((lam >= 0.0) ? -lam - t : -t);
 }

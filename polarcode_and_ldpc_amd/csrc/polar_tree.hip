@@ -207,6 +207,8 @@ template <int NL, int LCAP_, int F_, int DL_, int DS_ = 0>
 struct TG {
     static constexpr int n = NL, N = 1 << NL, LCAP = LCAP_, FPW = 64 / LCAP_, F = F_, DL = DL_;
     static constexpr int DS = DS_;  // dead-store record / replay instance (diagnostic, kernel comment)
+    // path-metric term form (metric_t): table (PL_METRIC_TAB), fused, or lean above PL_METRIC_FUSED_NMAX
+    static constexpr int MF = NL <= PL_METRIC_FUSED_NMAX ? (PL_METRIC_TAB ? 2 : 1) : 0;
     static constexpr int CW = N / 32;
     static constexpr int NB = n - 6;          // multi-word beta depths 1..NB (workspace)
     static constexpr bool STAGE = LCAP > 1;   // stage channel rows shared by a frame's lanes
@@ -632,7 +634,7 @@ PL_DEV void rate0_rest(const unsigned char* smem, const unsigned char* ws, int p
             for (int u = 0; u < IL; ++u) {
                 if (j0 + u < S) {
                     const double lam = ll[j0 + u];
-                    const double t = G::n <= PL_METRIC_FUSED_NMAX ? log1p_exp_neg(fabs(lam)) : log1p_pos(exp_neg(fabs(lam)));
+                    const double t = metric_t<G::MF>(fabs(lam));
                     inc[u] = (lam >= 0.0) ? -t : lam - t;
                 }
             }
@@ -695,6 +697,18 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
     uint32_t* const walk0 = reinterpret_cast<uint32_t*>(ws + G::W_WALK) + (G::SHADOW ? fw : 0);  // [2][CW][64]
 
     unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // STAMPS: metric evaluations -- [0] path_metrics_fast calls (per wave), [1] of
+    // them with a lane that needs log1p(e^-x), [2] such lanes, [3] active lanes
+    unsigned long long mcnt[4] = {0, 0, 0, 0};
+    auto count_metric = [&](double pmv, double lamv, bool act) {
+        if constexpr (STAMPS) {
+            const uint64_t need = __ballot(metric_needs_t(pmv, lamv, act)), on = __ballot(act);
+            mcnt[0] += 1;
+            mcnt[1] += need ? 1 : 0;
+            mcnt[2] += (unsigned long long)__popcll(need);
+            mcnt[3] += (unsigned long long)__popcll(on);
+        }
+    };
     unsigned long long tprev = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 #define STAMP(k)                                                    \
     if constexpr (STAMPS) {                                         \
@@ -868,13 +882,15 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
                 STAMP(3);
             } else if (frozen) {
                 double m0, m1;
-                path_metrics_fast<false, (G::n <= PL_METRIC_FUSED_NMAX)>(pm, lam, slot < nact, m0, m1);
+                count_metric(pm, lam, slot < nact);
+                path_metrics_fast<false, G::MF>(pm, lam, slot < nact, m0, m1);
                 if (slot < nact) pm = m0;
                 bit = 0;
                 STAMP(3);
             } else {
                 double m0, m1;
-                path_metrics_fast<true, (G::n <= PL_METRIC_FUSED_NMAX)>(pm, lam, slot < nact, m0, m1);
+                count_metric(pm, lam, slot < nact);
+                path_metrics_fast<true, G::MF>(pm, lam, slot < nact, m0, m1);
                 STAMP(3);
                 // a full, ordered list keeps its order: survivor s = path s
                 // with its better bit (ordered_prune), nothing exchanged
@@ -1265,8 +1281,10 @@ polar_tree_kernel(const double* __restrict__ llr, int64_t ld, uint8_t* __restric
 #endif
     }
     if constexpr (STAMPS && !DS) {
-        if (lane == 0)
+        if (lane == 0) {
             for (int k = 0; k < 8; ++k) atomicAdd(stamps + k, acc[k]);
+            for (int k = 0; k < 4; ++k) atomicAdd(stamps + 8 + k, mcnt[k]);
+        }
     }
 #undef STAMP
 }

@@ -57,45 +57,77 @@ def test_ms_504(gpu):
     assert np.array_equal(b, d["bp_bits"]) and np.array_equal(i, d["bp_iters"])
 
 
-@pytest.mark.parametrize("kernel", ["default", "generic"])
+@pytest.mark.parametrize("kernel", ["default", "compact", "generic"])
 def test_ms_8192(gpu, kernel, monkeypatch):
-    """n=8192: T/C do not fit LDS.  Default: min-sum with the compressed check
-    state in LDS (ldpc_ms_compact_kernel); generic: T/C in a global workspace."""
-    if kernel == "generic":
-        monkeypatch.setenv("PL_LDPC_KERNEL", "generic")
+    """n=8192: T/C do not fit LDS.  Default: the (3,6)-regular min-sum kernel
+    (ldpc_ms36_kernel, rebuild-ready check state); compact: the compressed check
+    state kernel (ldpc_ms_compact_kernel); generic: T/C in a global workspace."""
+    if kernel != "default":
+        monkeypatch.setenv("PL_LDPC_KERNEL", kernel)
     d = golden("ldpc_ms_8192.npz")
     dec = _L().MSDecoder(_H(d), max_iter=20, normalization=0.75)
     if kernel == "generic":
         assert dec.plan.info.lds_bytes < 64 * 1024 and dec.plan.info.reserved == 1
     else:
-        assert dec.plan.info.reserved == 5
+        assert dec.plan.info.reserved == (8 if kernel == "default" else 5)
     assert np.array_equal(dec.decode_batch(d["llr"]), d["ms_0_75"])
 
 
-@pytest.mark.parametrize("norm,es", [(0.75, True), (1.0, False)])
-def test_ms_compact_vs_oracle(gpu, oracle, norm, es):
-    """The compressed-state min-sum kernel on an n=8192 code against the oracle,
-    including exact zeros, +-inf and NaN LLRs (edge cases of its statistics)."""
-    L = _L()
-    H = L.regular_construction(8192, 3, 6, seed=1)
-    rp, ci = L.dense_to_csr(H)
-    rng = np.random.RandomState(17)
-    B = 24
+def _special_llrs(rng, B, n):
+    """Noisy all-zero-codeword LLRs with the special values of min-sum's check
+    statistics: exact zeros (one or many per check), -0, +-inf, NaN (one, a few)."""
     snr = rng.uniform(0.5, 2.5, size=(B, 1))
     sigma = np.sqrt(1.0 / (2.0 * 10 ** (snr / 10.0)))
-    llr = 2.0 * (1.0 + sigma * rng.randn(B, 8192)) / sigma ** 2
+    llr = 2.0 * (1.0 + sigma * rng.randn(B, n)) / sigma ** 2
     llr[1, ::5] = 0.0
     llr[2, ::97] = -0.0
     llr[3, 7] = np.nan
     llr[4, 11], llr[4, 12] = np.inf, -np.inf
     llr[5, :3] = np.nan
+    llr[6, rng.rand(n) < 0.3] = 0.0          # erasures: checks with 1, 2 or more zeros
+    llr[7, rng.rand(n) < 0.02] = np.nan      # scattered NaN
+    llr[8, rng.rand(n) < 0.1] = np.inf
+    llr[8, rng.rand(n) < 0.1] = -np.inf
+    llr[9, :] = np.where(rng.rand(n) < 0.5, 0.0, -0.0)
+    return llr
+
+
+@pytest.mark.parametrize("kernel", ["default", "compact"])
+@pytest.mark.parametrize("norm,es", [(0.75, True), (1.0, False), (-0.5, True), (1.25, False), (0.0, True)])
+def test_ms_compact_vs_oracle(gpu, oracle, monkeypatch, kernel, norm, es):
+    """The LDS-state min-sum kernels on an n=8192 (3,6)-regular code against the
+    oracle, including exact zeros, +-inf and NaN LLRs (edge cases of the check
+    statistics) and normalizations outside (0, 1]."""
+    if kernel != "default":
+        monkeypatch.setenv("PL_LDPC_KERNEL", kernel)
+    L = _L()
+    H = L.regular_construction(8192, 3, 6, seed=1)
+    rp, ci = L.dense_to_csr(H)
+    rng = np.random.RandomState(17)
+    llr = _special_llrs(rng, 24, 8192)
     want_b, want_i = oracle.ldpc_decode(rp, ci, 8192, llr, algo="ms", max_iter=20, early_stop=es, norm=norm,
                                         threads=8)
     dec = L.MSDecoder(H, 20, norm, es)
-    assert dec.plan.info.reserved == 5
+    assert dec.plan.info.reserved == (8 if kernel == "default" else 5)
     got_b, got_i = dec.decode_batch(llr, return_iterations=True)
     assert np.array_equal(got_b, want_b)
     assert np.array_equal(got_i, want_i)
+
+
+@pytest.mark.parametrize("n", [2048, 4096])
+def test_ms36_smaller_codes_vs_oracle(gpu, oracle, n):
+    """ldpc_ms36_kernel's n = 2048 / 4096 instances (one / two checks per thread)."""
+    L = _L()
+    H = L.regular_construction(n, 3, 6, seed=n)
+    rp, ci = L.dense_to_csr(H)
+    llr = _special_llrs(np.random.RandomState(n), 16, n)
+    for norm, es in ((0.75, True), (1.0, False)):
+        want_b, want_i = oracle.ldpc_decode(rp, ci, n, llr, algo="ms", max_iter=20, early_stop=es, norm=norm,
+                                            threads=8)
+        dec = L.MSDecoder(H, 20, norm, es)
+        assert dec.plan.info.reserved == 8
+        got_b, got_i = dec.decode_batch(llr, return_iterations=True)
+        assert np.array_equal(got_b, want_b) and np.array_equal(got_i, want_i), (norm, es)
 
 
 def test_ms_degree1_raises_like_reference(gpu):

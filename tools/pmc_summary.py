@@ -31,11 +31,11 @@ KEYS = {
     "ldpc_bp_504": ("g1", "pl::ldpc_bp_grp_kernel<3, 6, 2, false>", 65536),
     "polar_cascl_1024_l32": ("g1", "pl::polar_tree_kernel<10, 32, false, 3, 7, false, 4, 0>", 65536),
     "polar_scl_4096_l8": ("g1", "pl::polar_tree_kernel<12, 8, false, 4, 9, false, 4, 0>", 131072),
-    "ldpc_ms_8192_noes": ("g1", "pl::ldpc_ms_compact_kernel", 131072),
+    "ldpc_ms_8192_noes": ("g1", "pl::ldpc_ms", 131072),
     "polar_scl_1024_l8_default": ("g2", "pl::polar_tree_kernel<10, 8, false, 3, 7, false, 4, 0>", 65536),
     "polar_sc_1024_default": ("g2", "pl::polar_tree_kernel<10, 1, true, 1, 5, false, 2, 0>", 65536),
     "polar_sc_256": ("g2", "pl::polar_tree_kernel<8, 1, true, 1, 3, false, 2, 0>", 100),
-    "ldpc_ms_8192": ("g2", "pl::ldpc_ms_compact_kernel", 131072),
+    "ldpc_ms_8192": ("g2", "pl::ldpc_ms", 131072),
     "ldpc_bp_504_valid": ("g2", "pl::ldpc_bp_grp_kernel<3, 6, 2, false>", 65536),
 }
 PASSES = ("fetch", "write", "valu", "mix", "l2", "wait")

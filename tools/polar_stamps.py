@@ -22,12 +22,19 @@ msg = torch.empty((a.batch, K), dtype=torch.uint8, device="cuda"); _native.rando
 cw = torch.empty((a.batch, N), dtype=torch.uint8, device="cuda"); _native.polar_encode(plan, msg, cw)
 llr = AWGNChannel(a.snr).llr_batch_device(cw, N, a.batch, seed=42)
 out = torch.empty((a.batch, K), dtype=torch.uint8, device="cuda")
-st = torch.zeros(8, dtype=torch.int64, device="cuda")
+st = torch.zeros(16, dtype=torch.int64, device="cuda")
 plan.decode_stamped(llr, out, st); torch.cuda.synchronize(); st.zero_()
 t = time.perf_counter(); plan.decode_stamped(llr, out, st); torch.cuda.synchronize(); dt = time.perf_counter() - t
-s = st.cpu().numpy().astype(float)
+s_all = st.cpu().numpy().astype(float)
+s, mc = s_all[:8], s_all[8:12]
 ok = bool(torch.equal(out, msg)) if a.snr > 20 else None
 names = ["fused_top", "ws_chains", "lds_chain", "metrics", "prune_clone", "beta_walk", "final", "ws_sync"] if plan.info.reserved == 4 else ["llr_update", "metrics", "prune_clone", "beta_walk", "final"]
 print(json.dumps({"N": N, "L": a.list_size, "fused": plan.info.fused_top, "lds": plan.info.lds_bytes,
                   "stamped_ms": dt * 1e3, "cycles_per_frame": s.sum() / a.batch,
-                  "share": {k: round(v / s.sum(), 4) for k, v in zip(names, s)}}))
+                  "share": {k: round(v / s.sum(), 4) for k, v in zip(names, s)},
+                  # tree kernel: per-wave path_metrics_fast calls, those with a lane needing
+                  # log1p(e^-x), such lanes and active lanes (stamps[8..11])
+                  "metric_calls": mc[0], "metric_calls_evaluating": mc[1],
+                  "metric_lanes_evaluating": mc[2], "metric_lanes_active": mc[3],
+                  "wave_eval_fraction": round(mc[1] / max(1.0, mc[0]), 4),
+                  "lane_eval_fraction_of_active": round(mc[2] / max(1.0, mc[3]), 4)}))

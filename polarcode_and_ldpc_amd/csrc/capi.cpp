@@ -453,6 +453,7 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
         const size_t lds = (base + pl::ldpc_reg_list_bytes(g.reg_variant) + 15) & ~(size_t)15;
         if (tl < 65536 && lds <= 64 * 1024) {
             g.grp = 1;
+            g.fpg = env_int("PL_BP_FPG", 1) == 2 ? 2 : 1;  // frames per workgroup (A/B knob)
             g.tl = tl;
             g.lds_bytes = (int)lds;
             // sorted slot s goes to the thread slot (j = s / 4, wavefront w) in snake

@@ -135,6 +135,7 @@ struct LdpcGeom {
     int tl;            // grp: length of the padded T'/C' arrays (doubles)
     int npad;          // grp: pad positions listed after the variable slots (a multiple of 256, -1 filled)
     int ms36;          // > 0: ldpc_ms36_kernel<ms36> ((3,6)-regular min-sum, n = 1024 ms36)
+    int fpg;           // grp: frames per workgroup (1 or 2)
 };
 struct LdpcDev {
     const int32_t* row_ptr;   // [m+1]

@@ -514,7 +514,10 @@ PL_DEV double grp_prod(const double* tb, int i) {
 // STAMPS (diagnostic build): per-phase s_memtime cycles of every wavefront,
 // summed into stamps[wavefront][8] (init, vote, check pass, its barrier,
 // variable pass, tanh list, closing barrier, output).
-template <int DV, int EPT, int VPT, bool STAMPS = false>
+// FPG frames per workgroup, one after the other: the frame-independent tables
+// (edge slots, variable slots, pads) are loaded / written once per workgroup
+// and the next frame's channel LLRs are fetched while the current one decodes.
+template <int DV, int EPT, int VPT, bool STAMPS = false, int FPG = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
                    uint8_t* __restrict__ bits, int32_t* __restrict__ iters, int64_t batch,
@@ -529,8 +532,8 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
     }
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NT = 256;
-    const int64_t frame = blockIdx.x;
-    if (frame >= batch) return;
+    const int64_t frame0 = (int64_t)blockIdx.x * FPG;
+    if (frame0 >= batch) return;
     const int tid = threadIdx.x;
     const int n = g.n, m = g.m, tl = g.tl;
     double* T = reinterpret_cast<double*>(smem);  // T'[tl]: check inputs, per check, padded
@@ -541,7 +544,6 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
     const int mp = (m + 3) & ~3;
     uint32_t* syn = reinterpret_cast<uint32_t*>(smem + (size_t)16 * tl);  // [mp]
     uint16_t* work = reinterpret_cast<uint16_t*>(smem + (((size_t)16 * tl + (size_t)4 * mp + 15) & ~(size_t)15));
-    const double* __restrict__ ch = llr + frame * ld;
     const int lane = __lane_id();
 
     int meta[EPT];  // T' position of the edge's check | position in the check << 16 | D_s << 20
@@ -553,7 +555,7 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
     // variables by thread slot q = tid + 256 j (host-chosen order):
     // var_tpos = [T' positions of the slot's DV edges][their checks][variable or -1]
     int ve[VPT][DV], vc[VPT][DV], vid[VPT];
-    double chv[VPT];
+    double chv[VPT], nchv[FPG > 1 ? VPT : 1];
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
         const int q = tid + j * NT;
@@ -564,10 +566,8 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
             ve[j][k] = dv.var_tpos[q * DV + k];
             vc[j][k] = dv.var_tpos[DV * NT * VPT + q * DV + k];
         }
-        chv[j] = ok ? ch[vid[j]] : 0.0;
+        chv[j] = ok ? llr[frame0 * ld + vid[j]] : 0.0;
     }
-    for (int c = tid; c < mp; c += NT) syn[c] = 0u;  // H * 0
-    uint32_t decs = 0;  // bit j: the decision of variable tid + 256 j (initially 0)
     {
         // the pads (positions no edge writes: no barrier before the edges' writes)
         const int32_t* __restrict__ pads = dv.var_tpos + (2 * DV + 1) * NT * VPT;
@@ -576,6 +576,16 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
             if (x >= 0) T[x] = 1.0;
         }
     }
+  for (int fk = 0; fk < FPG; ++fk) {
+    const int64_t frame = frame0 + fk;
+    if (frame >= batch) break;  // workgroup-uniform
+    if (fk > 0) {
+        __syncthreads();  // every wavefront is done with the previous frame's T', C', syndrome
+#pragma unroll
+        for (int j = 0; j < VPT; ++j) chv[j] = nchv[j];
+    }
+    for (int c = tid; c < mp; c += NT) syn[c] = 0u;  // H * 0
+    uint32_t decs = 0;  // bit j: the decision of variable tid + 256 j (initially 0)
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
         if (vid[j] >= 0) {
@@ -588,6 +598,12 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
         }
     }
     __syncthreads();
+    if constexpr (FPG > 1) {  // the next frame's channel LLRs, in flight while this one decodes
+        if (frame + 1 < batch && fk + 1 < FPG) {
+#pragma unroll
+            for (int j = 0; j < VPT; ++j) nchv[j] = vid[j] >= 0 ? llr[(frame + 1) * ld + vid[j]] : 0.0;
+        }
+    }
     PL_GSTAMP(0)
     int done = g.max_iter;
     for (int it = 0; it < g.max_iter; ++it) {
@@ -699,6 +715,7 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
     for (int j = 0; j < VPT; ++j)
         if (vid[j] >= 0) o[vid[j]] = (uint8_t)((decs >> j) & 1u);
     if (iters && tid == 0) iters[frame] = done;
+  }
     PL_GSTAMP(7)
     if constexpr (STAMPS) {
         if (lane == 0)
@@ -708,12 +725,12 @@ ldpc_bp_grp_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64
 }
 
 // (DV, EPT, VPT) instances of ldpc_reg_kernel: E <= 256*EPT, n <= 256*VPT
-struct RegVariant { int dv, ept, vpt; void* k[3]; };  // BP, MS, BP degree-grouped
+struct RegVariant { int dv, ept, vpt; void* k[4]; };  // BP, MS, BP degree-grouped (1, 2 frames per group)
 template <int DV, int EPT, int VPT>
 static RegVariant reg_variant() {
     return {DV, EPT, VPT,
             {(void*)ldpc_reg_kernel<0, DV, EPT, VPT>, (void*)ldpc_reg_kernel<1, DV, EPT, VPT>,
-             (void*)ldpc_bp_grp_kernel<DV, EPT, VPT>}};
+             (void*)ldpc_bp_grp_kernel<DV, EPT, VPT>, (void*)ldpc_bp_grp_kernel<DV, EPT, VPT, false, 2>}};
 }
 static const RegVariant* reg_table(int& count) {
     // E = DV n for a constant variable degree, so (3, 8, 2) and (3, 16, 4) could
@@ -1525,7 +1542,7 @@ static void* pick_kernel(const LdpcGeom& g) {
     }
     if (g.reg_variant) {
         int cnt;
-        return reg_table(cnt)[g.reg_variant - 1].k[g.algo != 0 ? 1 : (g.grp ? 2 : 0)];
+        return reg_table(cnt)[g.reg_variant - 1].k[g.algo != 0 ? 1 : (g.grp ? (g.fpg == 2 ? 3 : 2) : 0)];
     }
 #if PL_DIAG
     if (g.check_kernel) return g.algo == 0 ? (void*)ldpc_check_kernel<0> : (void*)ldpc_check_kernel<1>;
@@ -1564,7 +1581,8 @@ hipError_t ldpc_launch(const LdpcGeom& g, const LdpcDev& d, const double* llr, i
     LdpcDev dd = d;
     void* args[] = {&gg, &dd, (void*)&llr, (void*)&ld, (void*)&bits, (void*)&iters, (void*)&batch,
                     (void*)&work};
-    return hipLaunchKernel(k, dim3((unsigned)batch), dim3(g.threads), args, dyn_lds(g), s);
+    const int fpg = g.fpg > 1 ? g.fpg : 1;  // frames per workgroup
+    return hipLaunchKernel(k, dim3((unsigned)((batch + fpg - 1) / fpg)), dim3(g.threads), args, dyn_lds(g), s);
 }
 
 }  // namespace pl

@@ -44,6 +44,32 @@ def test_bp_zero_codeword_snrs(gpu):
     assert np.array_equal(b, d["es50_bits"]) and np.array_equal(i, d["es50_iters"])
 
 
+@pytest.mark.parametrize("fpg", ["1", "2"])
+def test_bp_frames_per_group(gpu, oracle, monkeypatch, fpg):
+    """ldpc_bp_grp_kernel decoding 1 or 2 frames per workgroup (PL_BP_FPG):
+    the golden frames in odd-sized batches (a last workgroup with one frame), and
+    a batch mixing frames that stop early with frames that never converge (the
+    workgroup's two frames end at different iterations), against the oracle."""
+    monkeypatch.setenv("PL_BP_FPG", fpg)
+    d = golden("ldpc_bp_504.npz")
+    L = _L()
+    H = _H(d)
+    dec = L.BPDecoder(H, max_iter=20)
+    assert dec.plan.info.reserved == 7
+    for B in (1, 7, 23):
+        bits, its = dec.decode_batch(d["harness_llr"][:B], return_iterations=True)
+        assert np.array_equal(bits, d["harness_bits"][:B]) and np.array_equal(its, d["harness_iters"][:B])
+    bits, its = dec.decode_batch(d["zero_llr"], return_iterations=True)
+    assert np.array_equal(bits, d["zero_bits"]) and np.array_equal(its, d["zero_iters"])
+    mix = np.empty((2 * 24 + 1, 504))
+    mix[0::2] = np.resize(d["zero_llr"][24:], (25, 504))  # the higher-SNR all-zero frames (early stop)
+    mix[1::2] = d["harness_llr"][:24]
+    rp, ci = L.dense_to_csr(H)
+    want_b, want_i = oracle.ldpc_decode(rp, ci, 504, mix, threads=8)
+    bits, its = dec.decode_batch(mix, return_iterations=True)
+    assert np.array_equal(bits, want_b) and np.array_equal(its, want_i)
+
+
 def test_ms_504(gpu):
     d = golden("ldpc_ms_504.npz")
     L = _L()

@@ -2,7 +2,6 @@
 // (ldpc.hip) and the polar path metrics (polar_common.hpp).
 #pragma once
 #include "common.hpp"
-#include "metric_table.hpp"
 
 namespace pl {
 
@@ -135,6 +134,10 @@ PL_DEV double log1p_pos(double x) {
 PL_DEV double log1p_exp_neg(double x) {
     constexpr double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
     const double u = exp_neg(x);
+    // (measured, not kept: lanes with x > 8 taking the log1p series u - u^2/2 +
+    // ... - u^6/6 instead of the log kernel -- correctly rounded, 7 VALU instead
+    // of ~25, but the per-lane branch cost the tree kernel registers: N = 1024 L =
+    // 8 5.34 -> 6.70 ms, profiles/r06_b/ab_split.log)
     const bool big = u > 0.41421356237309503;
     const double f = big ? 0.5 * (u - 1.0) : u;
     const double hfsq = 0.5 * f * f;
@@ -142,37 +145,6 @@ PL_DEV double log1p_exp_neg(double x) {
     const double R = lg_R(s * s);
     const double j = big ? 1.0 : 0.0;
     return j * LN2_HI - ((hfsq - (s * (hfsq + R) + j * LN2_LO)) - f);
-}
-
-// log1p(exp(-x)) for x >= 0 from the table of tools/gen_metric_table.py
-// (metric_table.hpp): x0 = j/16 the nearest table point, |x0 - x| <= 1/32
-// (exact), then t = log1p(e^-x0) + log1p(w), w = e^-x0/(1 + e^-x0) *
-// expm1(x0 - x) -- expm1 to degree 7, log1p to degree 8 (|w| < 0.016): 20
-// fp64 operations and one 16-byte gather instead of the fused form's ~45.
-// <= 1.53 ulp (one ulp more than the fused form's 1.72 at most; on 3 M
-// inputs, 25 % not correctly rounded against 23 %).  x >= 48: e^-x alone
-// (u < 2^-69, so log1p(u) rounds to u); NaN: NaN.
-PL_DEV double log1p_exp_neg_tab(double x) {
-    if (!(x < 48.0)) return exp_neg(x);
-    const double jd = __builtin_rint(x * 16.0);
-    const double q = fma(jd, 0.0625, -x);  // x0 - x, exact
-    double p = 1.0 / 5040.0;
-    p = fma(p, q, 1.0 / 720.0);
-    p = fma(p, q, 1.0 / 120.0);
-    p = fma(p, q, 1.0 / 24.0);
-    p = fma(p, q, 1.0 / 6.0);
-    p = fma(p, q, 0.5);
-    const double em = fma(p * q, q, q);  // expm1(x0 - x)
-    const double2 row = kMetricTab[(int)jd];
-    const double w = row.y * em;
-    double l = -1.0 / 8.0;
-    l = fma(l, w, 1.0 / 7.0);
-    l = fma(l, w, -1.0 / 6.0);
-    l = fma(l, w, 1.0 / 5.0);
-    l = fma(l, w, -1.0 / 4.0);
-    l = fma(l, w, 1.0 / 3.0);
-    l = fma(l, w, -0.5);
-    return row.x + fma(l * w, w, w);
 }
 
 }  // namespace pl

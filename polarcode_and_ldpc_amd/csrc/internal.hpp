@@ -10,11 +10,6 @@
 // de-duplicated fused top -- every tree instance (n <= 12) now uses it
 #define PL_METRIC_FUSED_NMAX 12
 #endif
-#ifndef PL_METRIC_TAB
-// 1: the tree instances evaluate log1p(exp(-x)) from a 770-row table
-// (log1p_exp_neg_tab, fp64_math.hpp) instead of the fused exp + log1p
-#define PL_METRIC_TAB 0
-#endif
 
 namespace pl {
 
@@ -88,9 +83,8 @@ int nan_redo_lds_bytes(int list_size);
 hipError_t nan_redo_prepare(int list_size);
 // path-metric evaluation of the list kernel whose frames are redone: the lane
 // kernel's path_metrics (libm-style log1p(exp(-x))), or the tree instances'
-// path_metrics_fast with the fused (n <= PL_METRIC_FUSED_NMAX) or lean form, or
-// the table form (PL_METRIC_TAB)
-enum RedoMetric { kRedoMetricLane = 0, kRedoMetricFused = 1, kRedoMetricLean = 2, kRedoMetricTab = 3 };
+// path_metrics_fast with the fused (n <= PL_METRIC_FUSED_NMAX) or lean form
+enum RedoMetric { kRedoMetricLane = 0, kRedoMetricFused = 1, kRedoMetricLean = 2 };
 hipError_t nan_redo_launch(const double* llr, int64_t ld, uint8_t* out, int64_t batch, int N, int K, int Lsz,
                            const uint32_t* frozen_dec, const int32_t* info_pos, const uint32_t* crc_g,
                            uint64_t* masks, int grid, int fpw, int metric, unsigned char* scratch,

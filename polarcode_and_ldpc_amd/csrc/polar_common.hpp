@@ -68,11 +68,10 @@ PL_DEV bool metric_needs_t(double pm, double lam, bool active) {
 // inactive list slots (their metrics are never read) and pm = +-inf with a
 // non-NaN LLR (t is finite, so pm + anything finite = pm as in the reference).
 // t = log1p(exp(-x)), x >= 0, in the list kernels' evaluations (fp64_math.hpp):
-// FORM 0 lean exp + log1p, 1 fused, 2 table
+// FORM 0 lean exp + log1p, 1 fused
 template <int FORM>
 PL_DEV double metric_t(double x) {
-    if constexpr (FORM == 2) return log1p_exp_neg_tab(x);
-    else if constexpr (FORM == 1) return log1p_exp_neg(x);
+    if constexpr (FORM == 1) return log1p_exp_neg(x);
     else return log1p_pos(exp_neg(x));
 }
 

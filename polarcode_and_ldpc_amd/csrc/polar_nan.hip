@@ -131,8 +131,7 @@ PL_DEV void redo_frame(const RedoArgs& a, int64_t frame, const Bufs& bf, unsigne
             for (int p = tid; p < nact; p += kRedoThreads) {
                 const double lam = bf.llr(phys[p])[dep_off(N, n)];
                 double m0, m1;
-                if (a.metric == kRedoMetricTab) path_metrics_fast<false, 2>(pm[p], lam, true, m0, m1);
-                else if (a.metric == kRedoMetricFused) path_metrics_fast<false, true>(pm[p], lam, true, m0, m1);
+                if (a.metric == kRedoMetricFused) path_metrics_fast<false, true>(pm[p], lam, true, m0, m1);
                 else if (a.metric == kRedoMetricLean) path_metrics_fast<false, false>(pm[p], lam, true, m0, m1);
                 else path_metrics<false>(pm[p], lam, m0, m1);
                 pm[p] = m0;
@@ -143,8 +142,7 @@ PL_DEV void redo_frame(const RedoArgs& a, int64_t frame, const Bufs& bf, unsigne
             for (int p = tid; p < nact; p += kRedoThreads) {
                 const double lam = bf.llr(phys[p])[dep_off(N, n)];
                 double m0, m1;
-                if (a.metric == kRedoMetricTab) path_metrics_fast<true, 2>(pm[p], lam, true, m0, m1);
-                else if (a.metric == kRedoMetricFused) path_metrics_fast<true, true>(pm[p], lam, true, m0, m1);
+                if (a.metric == kRedoMetricFused) path_metrics_fast<true, true>(pm[p], lam, true, m0, m1);
                 else if (a.metric == kRedoMetricLean) path_metrics_fast<true, false>(pm[p], lam, true, m0, m1);
                 else path_metrics<true>(pm[p], lam, m0, m1);
                 cand[p] = PsItem{m0, p, 0};             // path_metrics_0 (decoder.py:300-303)

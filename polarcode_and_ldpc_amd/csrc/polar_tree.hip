@@ -207,8 +207,11 @@ template <int NL, int LCAP_, int F_, int DL_, int DS_ = 0>
 struct TG {
     static constexpr int n = NL, N = 1 << NL, LCAP = LCAP_, FPW = 64 / LCAP_, F = F_, DL = DL_;
     static constexpr int DS = DS_;  // dead-store record / replay instance (diagnostic, kernel comment)
-    // path-metric term form (metric_t): table (PL_METRIC_TAB), fused, or lean above PL_METRIC_FUSED_NMAX
-    static constexpr int MF = NL <= PL_METRIC_FUSED_NMAX ? (PL_METRIC_TAB ? 2 : 1) : 0;
+    // path-metric term form (metric_t): fused, or lean above PL_METRIC_FUSED_NMAX.  (A
+    // table form -- 20 fp64 operations and a 16-byte gather from a 770-row
+    // table instead of ~45 -- measured 35 % slower at N = 1024 L = 8: the gather
+    // waits on a saturated memory system, profiles/r06_b/ab_tab.log)
+    static constexpr int MF = NL <= PL_METRIC_FUSED_NMAX ? 1 : 0;
     static constexpr int CW = N / 32;
     static constexpr int NB = n - 6;          // multi-word beta depths 1..NB (workspace)
     static constexpr bool STAGE = LCAP > 1;   // stage channel rows shared by a frame's lanes

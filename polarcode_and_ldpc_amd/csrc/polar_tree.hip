@@ -288,6 +288,11 @@ struct TG {
 #define PL_NT_CH 1
 #endif
     static constexpr bool NT_ST = PL_NT_ST >= 0 ? PL_NT_ST != 0 : n <= 10;
+#ifndef PL_NT_ST_DEPTHS
+#define PL_NT_ST_DEPTHS -1  // -1: NT_ST ? NTD : 0
+#endif
+    // the stores of the NTS shallowest workspace depths as nt stores
+    static constexpr int NTS = PL_NT_ST_DEPTHS >= 0 ? PL_NT_ST_DEPTHS : (NT_ST ? NTD : 0);
     // fused top from staged depth D0 with de-duplicated chunk reads: a chunk is
     // LCAP pairs of every frame, W / 2 = 2^(F-D0-1) of them per depth-F
     // element, and the depth-F array (2^(n-F) elements) must fill at least one
@@ -356,7 +361,7 @@ PL_DEV void fold(Fold<G>& st, double v, int idx, unsigned char* smem, unsigned c
         if (idx & 1) {
             double2* dst = reinterpret_cast<double2*>((D >= G::DL ? smem : ws) + G::llr_off(D));
             if (G::DS != 2 || !((st.skip >> D) & 1u)) {
-                if constexpr (G::NT_ST && D < G::F + G::NTD && D < G::DL) {
+                if constexpr (D < G::F + G::NTS && D < G::DL) {
                     double2* a = dst + (idx >> 1) * 64 + plane;
                     __builtin_nontemporal_store(st.pend[D], &a->x);
                     __builtin_nontemporal_store(v, &a->y);
@@ -1371,6 +1376,7 @@ const TreeEntry* tree_table(int* count) {
         make_entry<10, 1, true, 2, 7>(),
         make_entry<10, 1, true, 1, 6, false, PL_SC_WPE>(),
         make_entry<10, 1, true, 1, 4, false, PL_SC_WPE>(),
+        make_entry<12, 8, false, 4, 8>(),
 #endif
     };
     *count = (int)(sizeof(tab) / sizeof(tab[0]));

@@ -454,8 +454,11 @@ extern "C" int pl_ldpc_plan_create(int32_t m, int32_t n, const int32_t* row_ptr,
             g.grp = 1;
             // two frames per workgroup, one after the other (ldpc_bp_grp_kernel FPG):
             // valid codewords (early stop) 0.777 -> 0.742 ms per 65 536 frames, the
-            // harness frames (20 iterations) equal; PL_BP_FPG=1 restores one
-            g.fpg = env_int("PL_BP_FPG", 2) == 1 ? 1 : 2;
+            // harness frames (20 iterations) equal; PL_BP_FPG=1 restores one.  Only
+            // the (DV, EPT, VPT) = (3, 6, 2) instance: the larger ones' two-frame
+            // builds spill 24-41 more VGPRs than their one-frame builds
+            const bool fpg2 = maxdv == 3 && pl::ldpc_reg_ept(g.reg_variant) == 6;
+            g.fpg = env_int("PL_BP_FPG", fpg2 ? 2 : 1) == 1 ? 1 : 2;
             g.tl = tl;
             g.lds_bytes = (int)lds;
             // sorted slot s goes to the thread slot (j = s / 4, wavefront w) in snake

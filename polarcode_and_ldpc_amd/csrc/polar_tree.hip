@@ -67,6 +67,12 @@ namespace {
 // budget, 32 workspace pairs per g batch and the channel loop unrolled 16
 // (against 8 pairs / unroll 2: N=1024 -5 %, default set -4 %, N=256 -7 %,
 // N=4096 -12 %, bits identical; profiles/r03_e/ab_sc_knobs*.log)
+#ifndef PL_T12_WPE
+#define PL_T12_WPE 4  // the N = 4096 L = 8 instance's register budget (waves per SIMD)
+#endif
+#ifndef PL_DLX_WPE
+#define PL_DLX_WPE 4  // diagnostic tier entries (tree_table)
+#endif
 #ifndef PL_SC_WPE
 #define PL_SC_WPE 2  // SC instances: waves per SIMD their register budget is built for
 #endif
@@ -1348,7 +1354,7 @@ const TreeEntry* tree_table(int* count) {
         make_entry<10, 16, false, 3, 7>(),
         make_entry<10, 4, false, 3, 7>(),
         make_entry<11, 8, false, 3, 8>(),
-        make_entry<12, 8, false, 4, 9>(),  // N = 4096: F = 4 11.63 vs F = 3 11.89 ms (16 384 frames)
+        make_entry<12, 8, false, 4, 9, false, PL_T12_WPE>(),  // N = 4096: F = 4 11.63 vs F = 3 11.89 ms (16 384 frames)
         make_entry<8, 2, false, 3, 5>(),
         make_entry<8, 4, false, 3, 5>(),
         make_entry<8, 8, false, 3, 5>(),
@@ -1376,7 +1382,12 @@ const TreeEntry* tree_table(int* count) {
         make_entry<10, 1, true, 2, 7>(),
         make_entry<10, 1, true, 1, 6, false, PL_SC_WPE>(),
         make_entry<10, 1, true, 1, 4, false, PL_SC_WPE>(),
-        make_entry<12, 8, false, 4, 8>(),
+        // one LDS depth more than the product entries (PL_DLX_WPE: their register budget)
+        make_entry<12, 8, false, 4, 8, false, PL_DLX_WPE>(),
+        make_entry<12, 8, false, 4, 7, false, PL_DLX_WPE>(),
+        make_entry<11, 8, false, 3, 7, false, PL_DLX_WPE>(),
+        make_entry<10, 8, false, 3, 6, false, PL_DLX_WPE>(),
+        make_entry<10, 32, false, 3, 6, false, PL_DLX_WPE>(),
 #endif
     };
     *count = (int)(sizeof(tab) / sizeof(tab[0]));

@@ -10,6 +10,6 @@ if [ "$1" = "DIAG=1" ]; then DIAG=1; shift; fi
 SRC="$R/polarcode_and_ldpc_amd/_lib/obj"; [ $DIAG = 1 ] && SRC="$R/polarcode_and_ldpc_amd/_lib/obj_diag"
 OBJ="$R/build/obj_$NAME"
 rm -rf "$OBJ"; mkdir -p "$OBJ"; cp -p "$SRC"/*.o "$OBJ"/
-for s in "$@"; do rm -f "$OBJ/$s.o"; done
+for s in "$@"; do rm -f "$OBJ/$s.o" "$OBJ/$s.hip.o" "$OBJ/$s.cpp.o"; done
 make -s -C "$R/polarcode_and_ldpc_amd/csrc" -j8 DIAG=$DIAG OUT="$R/build/lib_$NAME.so" OBJDIR="$OBJ" EXTRA="$EXTRA"
 echo "built build/lib_$NAME.so"

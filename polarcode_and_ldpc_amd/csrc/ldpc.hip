@@ -1226,6 +1226,13 @@ Ms36State ms36_special(double x0, double x1, double x2, double x3, double x4, do
 #ifndef PL_MS36_CREG
 #define PL_MS36_CREG 0  // 1: check adjacency in registers (spills), 0: one 16-byte load per check
 #endif
+#ifndef PL_MS36_CHREG
+// 1: the channel LLRs in registers across iterations (125 VGPRs, no spills):
+// n = 8192 8.91 -> 8.34 ms per 16 384 frames and 84 -> ~10 GB of memory-side
+// traffic per 131 072 (re-read per iteration, the rows 64 KB apart missed L2 about
+// half the time); 0: re-read per iteration (profiles/r06_d/ab_chreg.log)
+#define PL_MS36_CHREG 1
+#endif
 template <int VPT>
 __global__ void __launch_bounds__(1024)
 ldpc_ms36_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t ld,
@@ -1247,8 +1254,13 @@ ldpc_ms36_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t
     const int32_t* __restrict__ ci = dv.col_idx;
     const uint4* __restrict__ vw = reinterpret_cast<const uint4*>(dv.ms_vw);
     const double norm = g.norm;
+    double chr[PL_MS36_CHREG ? VPT : 1];
 #pragma unroll
-    for (int j = 0; j < VPT; ++j) tot[tid + 1024 * j] = ch[tid + 1024 * j];
+    for (int j = 0; j < VPT; ++j) {
+        const double c0 = ch[tid + 1024 * j];
+        if constexpr (PL_MS36_CHREG) chr[j] = c0;
+        tot[tid + 1024 * j] = c0;
+    }
     // the tot byte addresses of the DC variables of checks tid + 1024 q, two per
     // word: in registers (PL_MS36_CREG) or read per check from the plan (ms_cw)
     uint32_t ccol[PL_MS36_CREG ? MQ : 1][DC / 2];
@@ -1375,9 +1387,9 @@ ldpc_ms36_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t
         }
         const int syn = it == 0 ? check_pass(std::integral_constant<bool, true>())
                                 : check_pass(std::integral_constant<bool, false>());
-        // the variable pass reads the channel row and its edge words again every
-        // iteration (L2): an opaque index keeps the compiler from holding them in
-        // registers across iterations (spilled: 40 VGPRs)
+        // the variable pass reads its edge words again every iteration (L2): an
+        // opaque index keeps the compiler from holding them in registers across
+        // iterations (with the channel values: spilled 40 VGPRs)
         int vt = tid;
         asm volatile("" : "+v"(vt));
         if (g.early_stop && it > 0) {
@@ -1392,7 +1404,7 @@ ldpc_ms36_kernel(LdpcGeom g, LdpcDev dv, const double* __restrict__ llr, int64_t
             const int v = tid + 1024 * j;
             const int vo = vt + 1024 * j;
             const uint4 wa = vw[2 * vo], wb = vw[2 * vo + 1];  // w0 w1 w2 ma0 | ma1 ma2 - -
-            const double chv = ch[vo];
+            const double chv = PL_MS36_CHREG ? chr[PL_MS36_CHREG ? j : 0] : ch[vo];
             const uint32_t w[3] = {wa.x, wa.y, wa.z}, ma[3] = {wa.w, wb.x, wb.y};
             double sum = 0.0;
 #pragma unroll

@@ -561,7 +561,10 @@ LDPC_KERNELS = {1: "ldpc_decode_kernel<BP>", 2: "ldpc_reg_kernel<BP,DV=3>", 3: "
 
 def ldpc_kernel_name(plan):
     """The kernel pl_plan_get_info's `reserved` names (capi.cpp pl_plan_get_info)."""
-    return LDPC_KERNELS.get(int(plan.info.reserved), "ldpc kernel id %d" % plan.info.reserved)
+    r = int(plan.info.reserved)
+    if r == 7:  # the degree-grouped BP kernel: frames per workgroup (FPG) as its last template argument
+        return "ldpc_bp_grp_kernel<3,6,2,false,%d>" % max(1, int(plan.info.frames_per_block))
+    return LDPC_KERNELS.get(r, "ldpc kernel id %d" % r)
 
 
 def bench_ldpc_valid(args, rt, pool, enc, plan, kname):

@@ -28,7 +28,7 @@ import sys
 # bench.py pmc key -> (section group, kernel-name prefix, frames per launch in gpu_profile.sh)
 KEYS = {
     "polar_scl_1024_l8": ("g1", "pl::polar_tree_kernel<10, 8, false, 3, 7, false, 4, 0>", 65536),
-    "ldpc_bp_504": ("g1", "pl::ldpc_bp_grp_kernel<3, 6, 2, false>", 65536),
+    "ldpc_bp_504": ("g1", "pl::ldpc_bp_grp_kernel<3, 6, 2, false", 65536),
     "polar_cascl_1024_l32": ("g1", "pl::polar_tree_kernel<10, 32, false, 3, 7, false, 4, 0>", 65536),
     "polar_scl_4096_l8": ("g1", "pl::polar_tree_kernel<12, 8, false, 4, 9, false, 4, 0>", 131072),
     "ldpc_ms_8192_noes": ("g1", "pl::ldpc_ms", 131072),
@@ -36,7 +36,7 @@ KEYS = {
     "polar_sc_1024_default": ("g2", "pl::polar_tree_kernel<10, 1, true, 1, 5, false, 2, 0>", 65536),
     "polar_sc_256": ("g2", "pl::polar_tree_kernel<8, 1, true, 1, 3, false, 2, 0>", 100),
     "ldpc_ms_8192": ("g2", "pl::ldpc_ms", 131072),
-    "ldpc_bp_504_valid": ("g2", "pl::ldpc_bp_grp_kernel<3, 6, 2, false>", 65536),
+    "ldpc_bp_504_valid": ("g2", "pl::ldpc_bp_grp_kernel<3, 6, 2, false", 65536),
 }
 PASSES = ("fetch", "write", "valu", "mix", "l2", "wait")
 F64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")

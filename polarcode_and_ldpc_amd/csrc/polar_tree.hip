@@ -79,6 +79,12 @@ namespace {
 #ifndef PL_SC_U
 #define PL_SC_U 32  // SC instances: workspace parent pairs in flight per g-chain batch
 #endif
+#ifndef PL_LIST_U
+#define PL_LIST_U 8  // list instances: workspace parent pairs in flight per g-chain batch
+#endif
+#ifndef PL_FT_UNR32
+#define PL_FT_UNR32 2  // L = 32: the fused top's element-loop unroll
+#endif
 #ifndef PL_SC_FUNROLL
 #define PL_SC_FUNROLL 16  // SC instances: unroll of the depth-1 loop over the channel
 #endif
@@ -395,7 +401,7 @@ PL_DEV double descend_g(unsigned char* smem, unsigned char* ws, int plane, int p
     uint32_t w = 0;
     if constexpr (Q > G::NB) w = beta_get<n>(Q, bb, bw5);
     const uint32_t* bsrc = reinterpret_cast<const uint32_t*>(ws + G::bl_off(Q <= G::NB ? Q : 1)) + bs;
-    constexpr int UM = G::LCAP == 1 ? PL_SC_U : 8;
+    constexpr int UM = G::LCAP == 1 ? PL_SC_U : PL_LIST_U;
     constexpr int U = SQ < UM ? SQ : UM;  // parent pairs in flight
 #pragma unroll 1
     for (int t0 = 0; t0 < SQ; t0 += U) {
@@ -472,7 +478,7 @@ PL_DEV double fused_loop(unsigned char* smem, unsigned char* ws, int lane, int f
             // the next chunk's prefetch: unconditional (the last chunk re-reads
             // itself; a conditional one made the compiler's wait for the words
             // above a vmcnt(0) on the path without it, draining the prefetch)
-            constexpr int UNR = G::LCAP == 16 ? 4 : 2;  // element-loop unroll (4 at L = 32: +20 %)
+            constexpr int UNR = G::LCAP == 16 ? 4 : (G::LCAP == 32 ? PL_FT_UNR32 : 2);  // element-loop unroll (4 at L = 32: +20 %)
             auto prefetch = [&]() {
                 const int cn = c + 1 < NCH ? c + 1 : c;
 #pragma unroll

@@ -143,6 +143,14 @@ int pl_plan_release(pl_plan* plan, void* stream);
 int pl_plan_workspace_stats(const pl_plan* plan, int64_t* streams, int64_t* bytes);
 
 int pl_plan_get_info(const pl_plan* plan, pl_plan_info* info);
+/* Build-defined extension (no reference counterpart): the largest batch a
+ * pl_decode of this polar plan runs on its small-batch tree instance (one more
+ * LDS depth and a 2-wave register budget, polar_tree.hip tree_table_small;
+ * bits identical to the product instance), 0 if it has none.  Such batches fit
+ * the device at 8 wavefronts per CU, where that instance is 6-15 % faster;
+ * larger ones run the product instance (16 per CU).  PL_TREE_SMALL=0 at plan
+ * creation turns it off. */
+int pl_polar_plan_small_batch(const pl_plan* plan, int64_t* max_frames);
 int pl_plan_destroy(pl_plan* plan);
 const char* pl_last_error(void);
 

@@ -25,7 +25,7 @@ EXPORTS = (
     "pl_count_errors", "pl_debug_polar_stamps", "pl_debug_ldpc_stamps", "pl_debug_polar_deadstore", "pl_polar_plan_set_crc", "pl_crc_append",
     "pl_rayleigh_llr", "pl_bsc", "pl_gf2_encode", "pl_decode_ws", "pl_plan_workspace_bytes",
     "pl_plan_release", "pl_plan_workspace_stats", "pl_debug_set_plan_device", "pl_debug_polar_fpw",
-    "pl_debug_polar_flagged",
+    "pl_debug_polar_flagged", "pl_polar_plan_small_batch",
 )
 
 
@@ -54,6 +54,7 @@ def _load(path=LIB_PATH):
     L.pl_plan_workspace_stats.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     L.pl_debug_set_plan_device.argtypes = [P, I32]
     L.pl_plan_get_info.argtypes = [P, ctypes.POINTER(PlanInfo)]
+    L.pl_polar_plan_small_batch.argtypes = [P, ctypes.POINTER(ctypes.c_int64)]
     L.pl_plan_destroy.argtypes = [P]
     L.pl_last_error.restype = ctypes.c_char_p
     L.pl_random_bits.argtypes = [ctypes.c_uint64, I64, I64, I32, P, P]
@@ -161,6 +162,12 @@ class Plan:
         n, b = ctypes.c_int64(), ctypes.c_int64()
         check(lib.pl_plan_workspace_stats(self._h, ctypes.byref(n), ctypes.byref(b)), "pl_plan_workspace_stats")
         return int(n.value), int(b.value)
+
+    def small_batch_frames(self) -> int:
+        """Largest batch decoded on the small-batch tree instance (0: none)."""
+        b = ctypes.c_int64()
+        check(lib.pl_polar_plan_small_batch(self._h, ctypes.byref(b)), "pl_polar_plan_small_batch")
+        return int(b.value)
 
     def workspace_bytes(self, batch: int) -> int:
         b = ctypes.c_int64()

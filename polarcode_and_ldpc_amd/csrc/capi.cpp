@@ -51,6 +51,11 @@ struct pl_plan {
     std::vector<int32_t> h_info;       // ascending info positions (host copy)
     bool tree = false;      // compile-time-geometry kernel (polar_tree.hip); else polar_lane.hip
     pl::TreeInfo tinfo{};
+    // the small-batch tree instance (polar_tree.hip tree_table_small): used for a
+    // decode whose wavefronts all fit the device at its occupancy, small_grid_max
+    bool tree_small = false;
+    pl::TreeInfo tinfo_small{};
+    int small_grid_max = 0;
     pl::LaneGeom lgeo{};
     int fpw = 1;            // frames per wavefront
     int lane_grid_max = 0;  // resident wavefronts (persistent grid)
@@ -303,6 +308,17 @@ extern "C" int pl_polar_plan_create(int32_t N, int32_t K, const uint8_t* frozen_
     p->lane_grid_max = per_cu * device_cus(p->device);
     const int waves_env = env_int("PL_POLAR_WAVES", 0);
     if (waves_env > 0) p->lane_grid_max = waves_env;
+    if (p->tree && waves_env <= 0 && pl::tree_lookup_small(n, lcap, p->sc, &p->tinfo_small) &&
+        p->tinfo_small.ws_bytes <= p->tinfo.ws_bytes && p->tinfo_small.fpw == p->fpw) {
+        // its slices fit the main instance's (the workspace is sized for that one)
+        int per_cu_small = 0;
+        if ((e = pl::tree_prepare(p->tinfo_small, &per_cu_small)) != hipSuccess) {
+            pl_plan_destroy(p);
+            return hipfail(e, "polar kernel prepare");
+        }
+        p->small_grid_max = std::min(per_cu_small * device_cus(p->device), p->lane_grid_max);
+        p->tree_small = p->small_grid_max > 0;
+    }
     if (!p->sc) {
         p->mask_bytes = p->generic ? 0 : pl::nan_mask_region(p->lane_grid_max);
         p->redo_unit = pl::nan_redo_unit(N, list_size);
@@ -647,6 +663,10 @@ static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld,
     if (p->kind == 0) {
         if (!p->tree && stamps) return fail(PL_EUNSUPPORTED, "stamps only for the tree kernel");
         const int64_t waves = (batch + p->fpw - 1) / p->fpw;
+        // every wavefront of the decode resident at the small instance's occupancy:
+        // that instance (not for the dead-store diagnostics, headline instance only)
+        const bool small = p->tree_small && waves <= p->small_grid_max && dg.ds_mode == 0;
+        const pl::TreeInfo& ti = small ? p->tinfo_small : p->tinfo;
         int64_t grid = std::min<int64_t>(waves, p->lane_grid_max);
         while (grid > 1 && polar_bytes(p, grid) > ws_bytes) grid = std::min<int64_t>(grid - 1, grid * ws_bytes / polar_bytes(p, grid));
         unsigned char* const base = (unsigned char*)ws;
@@ -664,7 +684,7 @@ static int decode_impl(pl_plan* p, const double* llr, int64_t batch, int64_t ld,
             uint8_t* o0 = bits + b0 * p->pg.K;
             hipError_t e;
             if (p->tree)
-                e = pl::tree_launch(p->tinfo, l0, ld, o0, p->d_frozen_dec, p->d_info_pos, nb, p->pg.K,
+                e = pl::tree_launch(ti, l0, ld, o0, p->d_frozen_dec, p->d_info_pos, nb, p->pg.K,
                                     p->sc ? 1 : p->list_size, slices, (int)grid, stamps, p->d_crc_g,
                                     p->sc ? (const void*)p->d_r0k : (const void*)masks, s, dg.ds_mode);
             else
@@ -1022,6 +1042,12 @@ extern "C" int pl_plan_get_info(const pl_plan* p, pl_plan_info* info) {
         // 8 (3,6)-regular min-sum with rebuild-ready check state
         info->reserved = p->lg.ms36 ? 8 : p->lg.compact ? 5 : (p->lg.check_kernel ? 3 : (p->lg.grp ? 7 : (p->lg.reg_variant ? 2 : 1)));
     }
+    return PL_OK;
+}
+
+extern "C" int pl_polar_plan_small_batch(const pl_plan* p, int64_t* max_frames) {
+    if (!p || !max_frames) return fail(PL_EINVAL, "NULL argument");
+    *max_frames = (p->kind == 0 && p->tree_small) ? (int64_t)p->small_grid_max * p->fpw : 0;
     return PL_OK;
 }
 

@@ -53,6 +53,9 @@ struct TreeInfo {
     int F, DL, fpw;
 };
 bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info);
+// a list instance for batches that fit the device at its 8 waves per CU (one
+// more LDS depth, 2-wave register budget), if (n, lcap) has one
+bool tree_lookup_small(int n, int lcap, bool sc, TreeInfo* info);
 // The tree and lane kernels' frame groups (FPW frames) past the first one per
 // wavefront come from a u32 counter in the kSchedBytes just before their
 // slices (polar_tree.hip, polar_lane.hpp); tree_launch / lane_launch zero it.

@@ -70,9 +70,6 @@ namespace {
 #ifndef PL_T12_WPE
 #define PL_T12_WPE 4  // the N = 4096 L = 8 instance's register budget (waves per SIMD)
 #endif
-#ifndef PL_DLX_WPE
-#define PL_DLX_WPE 4  // diagnostic tier entries (tree_table)
-#endif
 #ifndef PL_SC_WPE
 #define PL_SC_WPE 2  // SC instances: waves per SIMD their register budget is built for
 #endif
@@ -1388,13 +1385,26 @@ const TreeEntry* tree_table(int* count) {
         make_entry<10, 1, true, 2, 7>(),
         make_entry<10, 1, true, 1, 6, false, PL_SC_WPE>(),
         make_entry<10, 1, true, 1, 4, false, PL_SC_WPE>(),
-        // one LDS depth more than the product entries (PL_DLX_WPE: their register budget)
-        make_entry<12, 8, false, 4, 8, false, PL_DLX_WPE>(),
-        make_entry<12, 8, false, 4, 7, false, PL_DLX_WPE>(),
-        make_entry<11, 8, false, 3, 7, false, PL_DLX_WPE>(),
-        make_entry<10, 8, false, 3, 6, false, PL_DLX_WPE>(),
-        make_entry<10, 32, false, 3, 6, false, PL_DLX_WPE>(),
 #endif
+    };
+    *count = (int)(sizeof(tab) / sizeof(tab[0]));
+    return tab;
+}
+
+// Small-batch instances: one more LDS depth (DL - 1) and a 2-wave register
+// budget (no spills; the LDS allows 8 waves per CU).  A batch whose wavefronts
+// fit the device at 8 per CU runs at that occupancy either way, and then the
+// depth kept out of the workspace wins: A/B on one box, bits identical
+// (profiles/r06_d/ab_sb*.log): N=4096 L=8 16 384 / 8 192 frames 9.75 -> 8.34 /
+// 7.10 -> 6.41 ms, N=2048 16 384 4.05 -> 3.71, N=1024 L=8 16 384 1.88 -> 1.76,
+// L=32 4 096 1.70 -> 1.59.  Above one such pass the product entries win (N=4096
+// at 131 072 frames: 76.7 against 57.8 ms at 4 waves per SIMD, ab_dl12.log).
+const TreeEntry* tree_table_small(int* count) {
+    static const TreeEntry tab[] = {
+        make_entry<12, 8, false, 4, 8, false, 2>(),
+        make_entry<11, 8, false, 3, 7, false, 2>(),
+        make_entry<10, 8, false, 3, 6, false, 2>(),
+        make_entry<10, 32, false, 3, 6, false, 2>(),
     };
     *count = (int)(sizeof(tab) / sizeof(tab[0]));
     return tab;
@@ -1419,6 +1429,29 @@ bool tree_lookup(int n, int lcap, bool sc, TreeInfo* info) {
             info->fn_stamps = t[k].fn_stamps;
             info->fn_ds[0] = t[k].fn_ds[0];
             info->fn_ds[1] = t[k].fn_ds[1];
+            info->lds_bytes = t[k].lds;
+            info->ws_bytes = t[k].ws;
+            info->F = t[k].F;
+            info->DL = t[k].DL;
+            info->fpw = 64 / lcap;
+            return true;
+        }
+    return false;
+}
+
+// the small-batch instance for (n, lcap) if there is one (tree_table_small);
+// PL_TREE_SMALL=0 turns them off, as does a diagnostic tier choice (PL_TREE_F / DL / DLOFF)
+bool tree_lookup_small(int n, int lcap, bool sc, TreeInfo* info) {
+    const char* off = std::getenv("PL_TREE_SMALL");
+    if (sc || (off && std::atoi(off) == 0)) return false;
+    if (PL_DIAG && (std::getenv("PL_TREE_F") || std::getenv("PL_TREE_DL") || std::getenv("PL_TREE_DLOFF"))) return false;
+    int cnt = 0;
+    const TreeEntry* t = tree_table_small(&cnt);
+    for (int k = 0; k < cnt; ++k)
+        if (t[k].n == n && t[k].lcap == lcap && t[k].sc == sc) {
+            *info = TreeInfo{};
+            info->fn = t[k].fn;
+            info->fn_stamps = t[k].fn_stamps;
             info->lds_bytes = t[k].lds;
             info->ws_bytes = t[k].ws;
             info->F = t[k].F;

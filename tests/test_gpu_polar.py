@@ -572,6 +572,46 @@ def test_later_grid_passes_vs_oracle(gpu, oracle, L):
     assert 0 < (out != msg).any(dim=1).sum().item() < B
 
 
+@pytest.mark.parametrize("N,L,snr", [(4096, 8, 1.0), (2048, 8, 1.0), (1024, 8, 0.0), (1024, 32, -1.0)])
+def test_small_batch_instances(gpu, oracle, monkeypatch, N, L, snr):
+    """Batches that fit the device at 8 wavefronts per CU decode on the
+    small-batch tree instance (one more LDS depth, 2-wave register budget,
+    polar_tree.hip tree_table_small).  At its largest batch, one frame above it
+    (the product instance) and a ragged small batch, the bits equal those of a
+    plan without it (PL_TREE_SMALL=0), and a sample of frames equals the oracle."""
+    import torch
+    from polarcode_and_ldpc_amd import _native
+    from polarcode_and_ldpc_amd.channel import AWGNChannel
+    P = _P()
+    K = N // 2
+    fr = P.construct_frozen_set(N, K, 2.0)
+    dec = P.SCLDecoder(N, K, L, frozen_bits=fr)
+    S = dec.plan.small_batch_frames()
+    assert S > 0 and S % (64 // L) == 0
+    monkeypatch.setenv("PL_TREE_SMALL", "0")
+    ref = P.SCLDecoder(N, K, L, frozen_bits=fr)
+    assert ref.plan.small_batch_frames() == 0
+    B = S + 1
+    msg = torch.empty((B, K), dtype=torch.uint8, device="cuda")
+    _native.random_bits(93, 0, msg)
+    cw = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+    _native.polar_encode(dec.plan, msg, cw)
+    llr = AWGNChannel(snr).llr_batch_device(cw, N, B, seed=94)
+    for b in (S, B, 333):
+        a = torch.empty((b, K), dtype=torch.uint8, device="cuda")
+        r = torch.empty((b, K), dtype=torch.uint8, device="cuda")
+        dec.plan.decode(llr[:b], a)
+        ref.plan.decode(llr[:b], r)
+        torch.cuda.synchronize()
+        assert torch.equal(a, r), b
+    idx = torch.cat([torch.arange(0, 16), torch.arange(S - 16, S)]).cuda()
+    a = torch.empty((S, K), dtype=torch.uint8, device="cuda")
+    dec.plan.decode(llr[:S], a)
+    torch.cuda.synchronize()
+    want = oracle.scl_decode(N, L, fr, llr[idx].cpu().numpy(), threads=16)
+    assert _mismatch(a[idx].cpu().numpy(), want) == 0
+
+
 @pytest.mark.parametrize("N,L", [(1024, 8), (1024, 32), (4096, 8), (512, 4), (256, 0)])
 def test_one_plan_two_streams(gpu, N, L):
     """Plans are shared across streams (SURVEY §8 b ownership row): two batches

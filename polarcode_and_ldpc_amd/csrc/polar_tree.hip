@@ -1405,6 +1405,12 @@ const TreeEntry* tree_table_small(int* count) {
         make_entry<11, 8, false, 3, 7, false, 2>(),
         make_entry<10, 8, false, 3, 6, false, 2>(),
         make_entry<10, 32, false, 3, 6, false, 2>(),
+#ifdef PL_SMALL_MORE
+        make_entry<10, 16, false, 3, 6, false, 2>(),
+        make_entry<10, 4, false, 3, 6, false, 2>(),
+        make_entry<9, 8, false, 3, 5, false, 2>(),
+        make_entry<9, 16, false, 3, 5, false, 2>(),
+#endif
     };
     *count = (int)(sizeof(tab) / sizeof(tab[0]));
     return tab;

@@ -16,7 +16,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CASES = ("enc_1024", "enc_4096", "awgn_1024", "awgn_8192", "lane_2048_l32", "lane_1024_l64", "lane_512_l4", "lane_8192_l8", "lane_1024_l128", "polar_l8_128k", "polar_l32_64k", "polar_4096_128k", "polar_2048", "polar_l16", "polar_sc128", "polar_sc512", "polar_sc2048", "polar_sc4096", "polar_l8", "ldpc_bp", "ldpc_bp_valid", "polar_l32", "polar_4096", "ms_8192", "ms_8192_es", "ms_504", "polar_sc", "polar_sc_def", "polar_sc_def_128k", "polar_sc_def_256k",
-         "polar_sc256", "cascl_l32", "polar_4096_8k", "polar_2048_16k", "polar_l8_16k", "polar_l32_4k")
+         "polar_sc256", "cascl_l32", "polar_4096_8k", "polar_2048_16k", "polar_l8_16k", "polar_l32_4k",
+         "polar_l16_8k", "polar_l4_32k", "polar_512_16k", "polar_512_l16_8k")
 
 
 def worker(cases):
@@ -58,6 +59,8 @@ def worker(cases):
                             "polar_4096": (4096, 8, 16384, 1.0), "polar_sc": (1024, 0, 65536, 3.0),
                             "polar_4096_8k": (4096, 8, 8192, 1.0), "polar_2048_16k": (2048, 8, 16384, 1.0),
                             "polar_l8_16k": (1024, 8, 16384, 3.0), "polar_l32_4k": (1024, 32, 4096, 1.0),
+                            "polar_l16_8k": (1024, 16, 8192, 1.0), "polar_l4_32k": (1024, 4, 32768, 2.0),
+                            "polar_512_16k": (512, 8, 16384, 2.0), "polar_512_l16_8k": (512, 16, 8192, 1.0),
                             "polar_sc_def": (1024, 0, 65536, 3.0), "polar_sc_def_128k": (1024, 0, 131072, 3.0), "polar_sc_def_256k": (1024, 0, 262144, 3.0), "polar_sc256": (256, 0, 65536, 3.0),
                             "polar_sc128": (128, 0, 65536, 3.0), "polar_sc512": (512, 0, 65536, 3.0),
                             "polar_sc2048": (2048, 0, 32768, 3.0), "polar_sc4096": (4096, 0, 32768, 3.0)}[case]

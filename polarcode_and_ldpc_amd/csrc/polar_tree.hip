@@ -1397,7 +1397,9 @@ const TreeEntry* tree_table(int* count) {
 // depth kept out of the workspace wins: A/B on one box, bits identical
 // (profiles/r06_d/ab_sb*.log): N=4096 L=8 16 384 / 8 192 frames 9.75 -> 8.34 /
 // 7.10 -> 6.41 ms, N=2048 16 384 4.05 -> 3.71, N=1024 L=8 16 384 1.88 -> 1.76,
-// L=32 4 096 1.70 -> 1.59.  Above one such pass the product entries win (N=4096
+// L=32 4 096 1.70 -> 1.59, L=16 8 192 1.80 -> 1.59, L=4 32 768 2.17 -> 1.97,
+// N=512 L=8 16 384 0.857 -> 0.817, L=16 8 192 0.760 -> 0.713 (ab_smore.log).
+// Above one such pass the product entries win (N=4096
 // at 131 072 frames: 76.7 against 57.8 ms at 4 waves per SIMD, ab_dl12.log).
 const TreeEntry* tree_table_small(int* count) {
     static const TreeEntry tab[] = {
@@ -1405,12 +1407,10 @@ const TreeEntry* tree_table_small(int* count) {
         make_entry<11, 8, false, 3, 7, false, 2>(),
         make_entry<10, 8, false, 3, 6, false, 2>(),
         make_entry<10, 32, false, 3, 6, false, 2>(),
-#ifdef PL_SMALL_MORE
         make_entry<10, 16, false, 3, 6, false, 2>(),
         make_entry<10, 4, false, 3, 6, false, 2>(),
         make_entry<9, 8, false, 3, 5, false, 2>(),
         make_entry<9, 16, false, 3, 5, false, 2>(),
-#endif
     };
     *count = (int)(sizeof(tab) / sizeof(tab[0]));
     return tab;

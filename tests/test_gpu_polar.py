@@ -572,7 +572,8 @@ def test_later_grid_passes_vs_oracle(gpu, oracle, L):
     assert 0 < (out != msg).any(dim=1).sum().item() < B
 
 
-@pytest.mark.parametrize("N,L,snr", [(4096, 8, 1.0), (2048, 8, 1.0), (1024, 8, 0.0), (1024, 32, -1.0)])
+@pytest.mark.parametrize("N,L,snr", [(4096, 8, 1.0), (2048, 8, 1.0), (1024, 8, 0.0), (1024, 32, -1.0), (1024, 16, 0.0),
+                                       (1024, 4, 1.0), (512, 8, 1.0), (512, 16, 0.0)])
 def test_small_batch_instances(gpu, oracle, monkeypatch, N, L, snr):
     """Batches that fit the device at 8 wavefronts per CU decode on the
     small-batch tree instance (one more LDS depth, 2-wave register budget,
